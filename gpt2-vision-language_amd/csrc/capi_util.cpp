@@ -1,0 +1,34 @@
+// Thread-local error reporting shared by every libgvl entry point.
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+#include <string>
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+namespace gvl {
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+}  // namespace gvl
+
+extern "C" {
+const char* gvl_last_error(void) { return g_last_error.c_str(); }
+int gvl_abi_version(void) { return GVL_ABI_VERSION; }
+}

@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of libgvl.
+// bf16 is carried as raw 16-bit words (uint16_t) in memory; arithmetic is fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GVL_DEV __device__ __forceinline__
+
+typedef uint16_t bf16_t;
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4_t lds_short4_t;
+
+GVL_DEV float bf2f(uint32_t x) { return __uint_as_float(x << 16); }
+GVL_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
+  return __builtin_bit_cast(bf16_t, b);
+}
+GVL_DEV uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+GVL_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+GVL_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// 16x16x32 bf16 MFMA: D = A(16x32) * B(32x16) + C.
+// Lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]; D[4(l>>4)+r][l&15].
+GVL_DEV float4_t mfma16(const short8_t& a, const short8_t& b, const float4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Transposed LDS read (ds_read_b64_tr_b16): per 16-lane group, lane 4q+p supplies the
+// address of row q, cols 4p..4p+3 of a 4x16 block; lane i receives column i of rows 0..3.
+GVL_DEV short4_t lds_read_tr(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(lds_ptr));
+}
+
+GVL_DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+GVL_DEV float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+GVL_DEV float block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+template <int NT>
+GVL_DEV float block_max(float v, float* red) {
+  v = warp_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
+// GELU variants used by the reference: nn.GELU(approximate='tanh') in the GPT-2 MLP
+// (source/gpt2/train_gpt2.py:52) and exact-erf nn.GELU() in the Q-Former MLP
+// (source/gpt2_q_former/model.py:126-130).
+GVL_DEV float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+GVL_DEV float dgelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+GVL_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+GVL_DEV float dgelu_erf(float x) {
+  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) +
+         x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Counter-based RNG for dropout masks (splitmix64 finaliser over (seed, index)).
+GVL_DEV uint32_t rng_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+// keep with probability 1-p: compare against threshold p * 2^32
+GVL_DEV bool rng_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return rng_u32(seed, idx) >= thresh;
+}

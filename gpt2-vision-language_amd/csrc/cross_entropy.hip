@@ -1,0 +1,130 @@
+// Fused softmax cross-entropy over bf16 logits (fp32 math): one 256-thread block per
+// target row, the whole row held in registers (<= 32 x 16-B chunks per thread, V <= 65536),
+// so logits are read from HBM once and dlogits = softmax - onehot written once.
+// HBM-bound: 2*V (read) + 2*V (write) bytes per row.
+#include "common.h"
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+constexpr int CE_NT = 256;
+constexpr int CE_MAXC = 32;
+
+__global__ __launch_bounds__(CE_NT) void ce_row_kernel(
+    const bf16_t* __restrict__ logits, int64_t ldl, int64_t V, int64_t rpg, int64_t gstride,
+    int64_t roff, const int64_t* __restrict__ targets, const uint8_t* __restrict__ mask,
+    float* __restrict__ row_loss, bf16_t* __restrict__ dlogits, int64_t ldd) {
+  __shared__ float red[CE_NT / 64];
+  const int64_t r = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t lrow = (r / rpg) * gstride + roff + (r % rpg);
+  const bf16_t* src = logits + lrow * ldl;
+  bf16_t* dst = dlogits ? dlogits + r * ldd : nullptr;
+  const int64_t tgt = targets[r];
+  const bool valid = (tgt != -100) && (mask == nullptr || mask[r] != 0);
+  const int nch = (int)(V >> 3);
+  if (!valid) {
+    if (dst) {
+      for (int c = tid; c < nch; c += CE_NT)
+        *reinterpret_cast<uint4*>(dst + (int64_t)c * 8) = make_uint4(0, 0, 0, 0);
+    }
+    if (tid == 0) row_loss[r] = 0.f;
+    return;
+  }
+  uint4 buf[CE_MAXC];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < CE_MAXC; ++i) {
+    const int c = tid + i * CE_NT;
+    if (c < nch) {
+      buf[i] = *reinterpret_cast<const uint4*>(src + (int64_t)c * 8);
+      const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mx = fmaxf(mx, fmaxf(lo_bf(w[k]), hi_bf(w[k])));
+    }
+  }
+  mx = block_max<CE_NT>(mx, red);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CE_MAXC; ++i) {
+    const int c = tid + i * CE_NT;
+    if (c < nch) {
+      const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += __expf(lo_bf(w[k]) - mx) + __expf(hi_bf(w[k]) - mx);
+    }
+  }
+  s = block_sum<CE_NT>(s, red);
+  const float lse = mx + __logf(s);
+  if (tid == 0) row_loss[r] = lse - bf2f(src[tgt]);
+  if (dst) {
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int i = 0; i < CE_MAXC; ++i) {
+      const int c = tid + i * CE_NT;
+      if (c < nch) {
+        const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+        uint32_t o[4];
+        const int64_t base = (int64_t)c * 8;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float a = __expf(lo_bf(w[k]) - mx) * inv;
+          float b = __expf(hi_bf(w[k]) - mx) * inv;
+          if (base + 2 * k == tgt) a -= 1.f;
+          if (base + 2 * k + 1 == tgt) b -= 1.f;
+          o[k] = pack2(a, b);
+        }
+        *reinterpret_cast<uint4*>(dst + base) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void ce_finalize_kernel(const float* __restrict__ row_loss,
+                                                           const int64_t* __restrict__ targets,
+                                                           const uint8_t* __restrict__ mask,
+                                                           int64_t rows, int mask_mode,
+                                                           float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f, n = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 1024) {
+    const bool valid = (targets[r] != -100) && (mask == nullptr || mask[r] != 0);
+    if (valid) {
+      s += row_loss[r];
+      n += 1.f;
+    }
+  }
+  s = block_sum<1024>(s, red);
+  n = block_sum<1024>(n, red);
+  if (threadIdx.x == 0) {
+    float inv = mask_mode ? 1.f / fmaxf(n, 1.f) : 1.f / n;  // 0/0 -> nan like torch
+    out[0] = (n == 0.f && !mask_mode) ? __int_as_float(0x7fc00000) : s * inv;
+    out[1] = inv;
+  }
+}
+
+}  // namespace
+
+extern "C" int gvl_cross_entropy(const void* logits, int64_t ldl, int64_t rows, int64_t vocab,
+                                 int64_t rows_per_group, int64_t group_stride, int64_t row_offset,
+                                 const int64_t* targets, const uint8_t* mask, int32_t mask_mode,
+                                 float* row_loss, void* dlogits, int64_t ldd, float* out,
+                                 gvl_stream_t stream) {
+  GVL_REQUIRE(vocab % 8 == 0 && vocab / 8 <= (int64_t)CE_NT * CE_MAXC,
+              "gvl_cross_entropy: vocab=%lld must be a multiple of 8 and <= 65536", (long long)vocab);
+  GVL_REQUIRE(ldl % 8 == 0 && (!dlogits || ldd % 8 == 0), "gvl_cross_entropy: ld must be mult of 8");
+  GVL_REQUIRE(rows_per_group > 0, "gvl_cross_entropy: rows_per_group must be > 0");
+  GVL_REQUIRE(row_loss && out && targets, "gvl_cross_entropy: null buffer");
+  hipStream_t s = gvl::as_stream(stream);
+  if (rows > 0) {
+    hipLaunchKernelGGL(ce_row_kernel, dim3((unsigned)rows), dim3(CE_NT), 0, s,
+                       static_cast<const bf16_t*>(logits), ldl, vocab, rows_per_group, group_stride,
+                       row_offset, targets, mask, row_loss, static_cast<bf16_t*>(dlogits), ldd);
+    GVL_LAUNCH_CHECK("gvl_cross_entropy(rows)");
+  }
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(1024), 0, s, row_loss, targets, mask, rows,
+                     (int)mask_mode, out);
+  GVL_LAUNCH_CHECK("gvl_cross_entropy(finalize)");
+  return 0;
+}

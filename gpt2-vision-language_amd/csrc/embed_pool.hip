@@ -1,0 +1,164 @@
+// Embedding gather/scatter (K1) and CLIP-token pooling (K15). Both HBM-bound, 16-B
+// vector accesses, one wave (embedding) / one block (pool) per output row.
+#include "common.h"
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+// out[row(r)] = wte[idx[r]] + wpe[r % T]; row(r) = (r/T)*S + off + r%T.
+__global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx,
+                                                      const bf16_t* __restrict__ wte,
+                                                      const bf16_t* __restrict__ wpe,
+                                                      bf16_t* __restrict__ out, int64_t n, int64_t T,
+                                                      int C, int64_t S, int64_t off) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t t = r % T;
+  const int64_t orow = (r / T) * S + off + t;
+  const bf16_t* a = wte + idx[r] * (int64_t)C;
+  const bf16_t* b = wpe + t * (int64_t)C;
+  bf16_t* o = out + orow * (int64_t)C;
+  for (int c = lane * 8; c < C; c += 512) {
+    const uint4 u = *reinterpret_cast<const uint4*>(a + c);
+    const uint4 v = *reinterpret_cast<const uint4*>(b + c);
+    uint4 w;
+    w.x = pack2(lo_bf(u.x) + lo_bf(v.x), hi_bf(u.x) + hi_bf(v.x));
+    w.y = pack2(lo_bf(u.y) + lo_bf(v.y), hi_bf(u.y) + hi_bf(v.y));
+    w.z = pack2(lo_bf(u.z) + lo_bf(v.z), hi_bf(u.z) + hi_bf(v.z));
+    w.w = pack2(lo_bf(u.w) + lo_bf(v.w), hi_bf(u.w) + hi_bf(v.w));
+    *reinterpret_cast<uint4*>(o + c) = w;
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_bwd_kernel(const int64_t* __restrict__ idx,
+                                                      const bf16_t* __restrict__ dout,
+                                                      float* __restrict__ dwte,
+                                                      float* __restrict__ dwpe, int64_t n, int64_t T,
+                                                      int C, int64_t S, int64_t off) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t t = r % T;
+  const int64_t orow = (r / T) * S + off + t;
+  const bf16_t* g = dout + orow * (int64_t)C;
+  float* a = dwte ? dwte + idx[r] * (int64_t)C : nullptr;
+  float* b = dwpe ? dwpe + t * (int64_t)C : nullptr;
+  for (int c = lane * 2; c < C; c += 128) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(g + c);
+    const float g0 = lo_bf(u), g1 = hi_bf(u);
+    if (a) { atomicAdd(a + c, g0); atomicAdd(a + c + 1, g1); }
+    if (b) { atomicAdd(b + c, g0); atomicAdd(b + c + 1, g1); }
+  }
+}
+
+// Pool: block per (b, o), o in [0, 33): o=0 is CLS, o=1+i*8+j the adaptive-avg window
+// rows [floor(i*s/4), ceil((i+1)*s/4)), cols [floor(j*s/8), ceil((j+1)*s/8)); then the
+// 33 tokens are L2-normalised with F.normalize's max(||x||, 1e-12).
+constexpr int POOL_NT = 256;
+constexpr int POOL_MAXD = 4;  // D <= 1024
+
+template <typename TIn>
+GVL_DEV float ld_in(const TIn* p);
+template <>
+GVL_DEV float ld_in<float>(const float* p) { return *p; }
+template <>
+GVL_DEV float ld_in<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+
+template <typename TIn>
+__global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ in, void* out,
+                                                       int out_f32, int64_t L, int D, int side) {
+  __shared__ float red[POOL_NT / 64];
+  const int64_t b = blockIdx.y;
+  const int o = blockIdx.x;
+  const TIn* base = in + b * L * (int64_t)D;
+  float acc[POOL_MAXD];
+  int r0 = 0, r1 = 1, c0 = 0, c1 = 1;
+  if (o > 0) {
+    const int i = (o - 1) >> 3, j = (o - 1) & 7;
+    r0 = (i * side) / 4;
+    r1 = ((i + 1) * side + 3) / 4;
+    c0 = (j * side) / 8;
+    c1 = ((j + 1) * side + 7) / 8;
+  }
+  const float inv_cnt = 1.f / (float)((r1 - r0) * (c1 - c0));
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < POOL_MAXD; ++k) {
+    const int d = threadIdx.x + k * POOL_NT;
+    float a = 0.f;
+    if (d < D) {
+      if (o == 0) {
+        a = ld_in<TIn>(base + d);
+      } else {
+        for (int y = r0; y < r1; ++y)
+          for (int x = c0; x < c1; ++x) a += ld_in<TIn>(base + (1 + (int64_t)y * side + x) * D + d);
+        a *= inv_cnt;
+      }
+    }
+    acc[k] = a;
+    ss += a * a;
+  }
+  ss = block_sum<POOL_NT>(ss, red);
+  const float scale = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  const int64_t orow = (b * 33 + o) * (int64_t)D;
+#pragma unroll
+  for (int k = 0; k < POOL_MAXD; ++k) {
+    const int d = threadIdx.x + k * POOL_NT;
+    if (d < D) {
+      const float v = acc[k] * scale;
+      if (out_f32) reinterpret_cast<float*>(out)[orow + d] = v;
+      else reinterpret_cast<bf16_t*>(out)[orow + d] = f2bf(v);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int gvl_embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out,
+                                 int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
+                                 int64_t out_offset, gvl_stream_t stream) {
+  GVL_REQUIRE(C % 8 == 0, "gvl_embedding_fwd: C must be a multiple of 8");
+  GVL_REQUIRE(T > 0, "gvl_embedding_fwd: T must be > 0");
+  if (n_tokens == 0) return 0;
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3((unsigned)((n_tokens + 3) / 4)), dim3(256), 0,
+                     gvl::as_stream(stream), idx, static_cast<const bf16_t*>(wte),
+                     static_cast<const bf16_t*>(wpe), static_cast<bf16_t*>(out), n_tokens, T, (int)C,
+                     out_rows_per_seq, out_offset);
+  GVL_LAUNCH_CHECK("gvl_embedding_fwd");
+  return 0;
+}
+
+extern "C" int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc,
+                                 float* dwpe_acc, int64_t n_tokens, int64_t T, int64_t C,
+                                 int64_t out_rows_per_seq, int64_t out_offset, gvl_stream_t stream) {
+  GVL_REQUIRE(C % 2 == 0 && T > 0, "gvl_embedding_bwd: bad shape");
+  if (n_tokens == 0) return 0;
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)((n_tokens + 3) / 4)), dim3(256), 0,
+                     gvl::as_stream(stream), idx, static_cast<const bf16_t*>(dout), dwte_acc,
+                     dwpe_acc, n_tokens, T, (int)C, out_rows_per_seq, out_offset);
+  GVL_LAUNCH_CHECK("gvl_embedding_bwd");
+  return 0;
+}
+
+extern "C" int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
+                             int64_t B, int64_t L, int64_t D, gvl_stream_t stream) {
+  const int64_t N = L - 1;
+  int side = 0;
+  while ((int64_t)(side + 1) * (side + 1) <= N) ++side;
+  GVL_REQUIRE((int64_t)side * side == N && side > 0,
+              "gvl_pool_clip: expected square grid, got N=%lld", (long long)N);
+  GVL_REQUIRE(D > 0 && D <= POOL_NT * POOL_MAXD, "gvl_pool_clip: D=%lld unsupported", (long long)D);
+  if (B == 0) return 0;
+  dim3 grid(33, (unsigned)B);
+  hipStream_t s = gvl::as_stream(stream);
+  if (in_fp32)
+    hipLaunchKernelGGL(pool_kernel<float>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
+                       out, (int)out_fp32, L, (int)D, side);
+  else
+    hipLaunchKernelGGL(pool_kernel<bf16_t>, grid, dim3(POOL_NT), 0, s,
+                       static_cast<const bf16_t*>(in), out, (int)out_fp32, L, (int)D, side);
+  GVL_LAUNCH_CHECK("gvl_pool_clip");
+  return 0;
+}

@@ -1,0 +1,272 @@
+// bf16 GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_bf16) with a fused epilogue.
+//
+// Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave a 64x64 sub-tile of
+// 4x4 MFMA tiles.  Operands are register-staged through a double-buffered LDS image:
+//   K-contiguous operand  -> [128 rows][64 k]   128-B rows, 16-B chunk XOR (row>>1)&7,
+//                            fragments by ds_read_b128 (conflict-free for 16x16x32 maps);
+//   MN-contiguous operand -> [64 k][128 cols]   256-B rows, chunk XOR fT(k),
+//                            fragments by two ds_read_b64_tr_b16 (hardware transpose).
+// The MFMA is issued with operands swapped (B-fragment as "A") so each lane owns one
+// output row and four consecutive output columns -> 8-byte epilogue stores.
+// Workgroups are remapped so that consecutive tiles share an XCD (L2) — T1 of the guide.
+#include "common.h"
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int STAGE_BYTES = 2 * 16384;  // A image + B image
+
+struct GemmP {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  int64_t M, N, K, lda, ldb, ldc;
+  float alpha;
+  const float* alpha_ptr;
+  const bf16_t* bias;
+  bf16_t* pre_out;
+  const bf16_t* pre_in;
+  int64_t ldp;
+  const bf16_t* residual;
+  int64_t ldr;
+  const bf16_t* gate;
+  uint64_t seed;
+  float drop_scale;
+  uint32_t drop_thresh;
+  int tiles_m, tiles_n;
+  int act, dact, c_f32, has_drop;
+};
+
+GVL_DEV int swz_k(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+GVL_DEV int fT(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+GVL_DEV int swz_t(int krow, int chunk) { return krow * 256 + ((chunk ^ fT(krow)) << 4); }
+
+// Global -> registers for one 128x64 (or 64x128) operand tile.
+template <bool MN>
+GVL_DEV void load_tile(uint4 (&r)[4], const bf16_t* __restrict__ X, int64_t ld, int64_t r0,
+                       int64_t R, int64_t k0, int64_t K, int tid) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    int64_t row, col;
+    bool ok;
+    if (!MN) {
+      const int rr = (tid >> 3) + 32 * it, ch = tid & 7;
+      row = r0 + rr;
+      col = k0 + ch * 8;
+      ok = (row < R) && (col < K);
+    } else {
+      const int kr = (tid >> 4) + 16 * it, ch = tid & 15;
+      row = k0 + kr;
+      col = r0 + ch * 8;
+      ok = (row < K) && (col < R);
+    }
+    if (ok) {
+      r[it] = *reinterpret_cast<const uint4*>(X + row * ld + col);
+    } else {
+      r[it] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+template <bool MN>
+GVL_DEV void store_tile(const uint4 (&r)[4], char* lds, int tid) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    int off;
+    if (!MN) {
+      off = swz_k((tid >> 3) + 32 * it, tid & 7);
+    } else {
+      off = swz_t((tid >> 4) + 16 * it, tid & 15);
+    }
+    *reinterpret_cast<uint4*>(lds + off) = r[it];
+  }
+}
+
+// Fragment of a 16(row) x 32(k) operand slab: rows/cols [c0, c0+16), k-step s (k 32s..32s+31).
+template <bool MN>
+GVL_DEV short8_t read_frag(const char* lds, int c0, int s, int lane) {
+  if (!MN) {
+    const int row = c0 + (lane & 15), ch = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const short8_t*>(lds + swz_k(row, ch));
+  } else {
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int krow = 32 * s + 8 * G + q;
+    const int ch = (c0 >> 3) + (p >> 1);
+    const int f = fT(krow);
+    const int off1 = krow * 256 + ((ch ^ f) << 4) + (p & 1) * 8;
+    const int off2 = off1 + 4 * 256;  // krow+4 has the same fT
+    short4_t lo = lds_read_tr(lds + off1);
+    short4_t hi = lds_read_tr(lds + off2);
+    short8_t r;
+    r.lo = lo;
+    r.hi = hi;
+    return r;
+  }
+}
+
+template <bool AMN, bool BMN>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a
+  // contiguous range of tiles (row-major over (tm, tn)) so A panels are L2 hits.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  float4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((p.K + BK - 1) / BK);
+  uint4 ra[4], rb[4];
+  load_tile<AMN>(ra, p.A, p.lda, m0, p.M, 0, p.K, tid);
+  load_tile<BMN>(rb, p.B, p.ldb, n0, p.N, 0, p.K, tid);
+  store_tile<AMN>(ra, smem, tid);
+  store_tile<BMN>(rb, smem + 16384, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      load_tile<AMN>(ra, p.A, p.lda, m0, p.M, (int64_t)(kt + 1) * BK, p.K, tid);
+      load_tile<BMN>(rb, p.B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BK, p.K, tid);
+    }
+    const char* sa = smem + (kt & 1) * STAGE_BYTES;
+    const char* sb = sa + 16384;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      short8_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<AMN>(sa, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BMN>(sb, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+    }
+    if (more) {
+      char* dst = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      store_tile<AMN>(ra, dst, tid);
+      store_tile<BMN>(rb, dst + 16384, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns row m, columns n..n+3 of each 16x16 tile ----
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
+      if (p.bias) {
+        const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
+        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+      }
+      if (p.dact) {
+        const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
+        const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+      }
+      if (p.act) {
+        if (p.pre_out) {
+          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
+      }
+      if (p.has_drop) {
+        const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = rng_keep(p.seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
+      }
+      if (p.gate) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= gatev;
+      }
+      if (p.residual) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
+        v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+      }
+      if (p.c_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + m * p.ldc + n) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
+  GVL_REQUIRE(d != nullptr, "gvl_gemm: null descriptor");
+  GVL_REQUIRE(d->m >= 0 && d->n >= 0 && d->k >= 0, "gvl_gemm: negative size");
+  if (d->m == 0 || d->n == 0) return 0;
+  GVL_REQUIRE(d->a && d->b && d->c, "gvl_gemm: null operand");
+  GVL_REQUIRE(d->k % 8 == 0, "gvl_gemm: K=%lld must be a multiple of 8", (long long)d->k);
+  GVL_REQUIRE(d->n % 4 == 0, "gvl_gemm: N=%lld must be a multiple of 4", (long long)d->n);
+  GVL_REQUIRE(!d->a_mn || d->m % 8 == 0, "gvl_gemm: M must be a multiple of 8 for MN-major A");
+  GVL_REQUIRE(!d->b_mn || d->n % 8 == 0, "gvl_gemm: N must be a multiple of 8 for MN-major B");
+  GVL_REQUIRE(d->lda % 8 == 0 && d->ldb % 8 == 0 && d->ldc % 4 == 0,
+              "gvl_gemm: leading dims must be multiples of 8 (lda, ldb) / 4 (ldc)");
+  GVL_REQUIRE(gvl::aligned16(d->a) && gvl::aligned16(d->b) && gvl::aligned8(d->c),
+              "gvl_gemm: operands must be 16-byte aligned");
+  GVL_REQUIRE(d->act >= 0 && d->act <= 2 && d->dact >= 0 && d->dact <= 2, "gvl_gemm: bad act");
+  GVL_REQUIRE(!d->dact || (d->pre_in && d->ldp % 4 == 0), "gvl_gemm: dact needs pre_in");
+  GVL_REQUIRE(!d->residual || d->ldr % 4 == 0, "gvl_gemm: ldr must be a multiple of 4");
+  GVL_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "gvl_gemm: drop_p out of range");
+  GemmP p;
+  p.A = static_cast<const bf16_t*>(d->a);
+  p.B = static_cast<const bf16_t*>(d->b);
+  p.C = d->c;
+  p.M = d->m; p.N = d->n; p.K = d->k;
+  p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
+  p.alpha = d->alpha;
+  p.alpha_ptr = d->alpha_ptr;
+  p.bias = static_cast<const bf16_t*>(d->bias);
+  p.pre_out = static_cast<bf16_t*>(d->pre_out);
+  p.pre_in = static_cast<const bf16_t*>(d->pre_in);
+  p.ldp = d->ldp;
+  p.residual = static_cast<const bf16_t*>(d->residual);
+  p.ldr = d->ldr;
+  p.gate = static_cast<const bf16_t*>(d->gate);
+  p.seed = d->seed;
+  p.has_drop = d->drop_p > 0.f;
+  p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
+  p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
+  p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
+  p.tiles_m = (int)((d->m + BM - 1) / BM);
+  p.tiles_n = (int)((d->n + BN - 1) / BN);
+  const int grid = p.tiles_m * p.tiles_n;
+  hipStream_t s = gvl::as_stream(stream);
+  if (!d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, false>), dim3(grid), dim3(NT), 0, s, p);
+  else if (!d->a_mn && d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, true>), dim3(grid), dim3(NT), 0, s, p);
+  else if (d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<true, false>), dim3(grid), dim3(NT), 0, s, p);
+  else hipLaunchKernelGGL((gemm_bf16_kernel<true, true>), dim3(grid), dim3(NT), 0, s, p);
+  GVL_LAUNCH_CHECK("gvl_gemm");
+  return 0;
+}

@@ -1,0 +1,319 @@
+// Optimizer path over flat bf16 arenas + small fused elementwise helpers.
+//  - grad norm: grid-stride sum of squares (16-B loads) -> per-block partials -> one block
+//    finishes ||g|| and the clip coefficient on the device (no host sync);
+//  - AdamW: one streaming pass, p/g/m/v bf16 in, p/m/v bf16 out, fp32 opmath, the clip
+//    coefficient applied to g on the fly (torch _fused_adamw_ semantics, decoupled decay).
+// All HBM-bound: AdamW moves 14 B/param, the norm 2 B/param.
+#include "common.h"
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+constexpr int RED_NT = 256;
+constexpr int RED_MAXB = 1024;
+
+int red_blocks(int64_t n8) {
+  int64_t nb = (n8 + RED_NT - 1) / RED_NT;
+  if (nb > RED_MAXB) nb = RED_MAXB;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+GVL_DEV void unpack8(const uint4& u, float (&f)[8]) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+GVL_DEV uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+__global__ __launch_bounds__(RED_NT) void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n,
+                                                       float* __restrict__ partial) {
+  __shared__ float red[RED_NT / 64];
+  float s = 0.f;
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * RED_NT + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * RED_NT) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + i * 8), f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += f[k] * f[k];
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += RED_NT) {
+      const float v = bf2f(g[i]);
+      s += v * v;
+    }
+  }
+  s = block_sum<RED_NT>(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(RED_NT) void norm_finish_kernel(const float* __restrict__ partial,
+                                                             int nb, float max_norm,
+                                                             float* __restrict__ out) {
+  __shared__ float red[RED_NT / 64];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += RED_NT) s += partial[i];
+  s = block_sum<RED_NT>(s, red);
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(s);
+    out[0] = nrm;
+    out[1] = fminf(1.f, max_norm / (nrm + 1e-6f));
+  }
+}
+
+struct AdamP {
+  float lr, b1, b2, eps, wd, bc1, bc2_sqrt;
+};
+
+GVL_DEV void adam_elem(float& p, float g, float& m, float& v, const AdamP& a, bool decay) {
+  if (decay) p = p * (1.f - a.lr * a.wd);
+  m = a.b1 * m + (1.f - a.b1) * g;
+  v = a.b2 * v + (1.f - a.b2) * g * g;
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p - (a.lr / a.bc1) * m / denom;
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ p,
+                                                    const bf16_t* __restrict__ g,
+                                                    bf16_t* __restrict__ m, bf16_t* __restrict__ v,
+                                                    int64_t n, int64_t n_decay, AdamP a,
+                                                    const float* __restrict__ gscale) {
+  const float cs = gscale ? *gscale : 1.f;
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float fp[8], fg[8], fm[8], fv[8];
+    unpack8(*reinterpret_cast<const uint4*>(p + i * 8), fp);
+    unpack8(*reinterpret_cast<const uint4*>(g + i * 8), fg);
+    unpack8(*reinterpret_cast<const uint4*>(m + i * 8), fm);
+    unpack8(*reinterpret_cast<const uint4*>(v + i * 8), fv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // clip_grad_norm_ scales the bf16 grad in place before the step: round like it
+      const float gk = bf2f(f2bf(fg[k] * cs));
+      adam_elem(fp[k], gk, fm[k], fv[k], a, (i * 8 + k) < n_decay);
+    }
+    *reinterpret_cast<uint4*>(p + i * 8) = pack8(fp);
+    *reinterpret_cast<uint4*>(m + i * 8) = pack8(fm);
+    *reinterpret_cast<uint4*>(v + i * 8) = pack8(fv);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += 256) {
+      float fp = bf2f(p[i]), fm = bf2f(m[i]), fv = bf2f(v[i]);
+      const float gk = bf2f(f2bf(bf2f(g[i]) * cs));
+      adam_elem(fp, gk, fm, fv, a, i < n_decay);
+      p[i] = f2bf(fp); m[i] = f2bf(fm); v[i] = f2bf(fv);
+    }
+  }
+}
+
+// Column sums: block b sums rows [b*chunk, (b+1)*chunk) for all columns -> ws[b][cols].
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ x,
+                                                             int64_t rows, int64_t cols, int64_t ld,
+                                                             int64_t chunk, float* __restrict__ ws) {
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  int64_t r1 = r0 + chunk;
+  if (r1 > rows) r1 = rows;
+  for (int64_t c = threadIdx.x * 2; c < cols; c += 512) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int64_t r = r0; r < r1; ++r) {
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(x + r * ld + c);
+      s0 += lo_bf(u);
+      s1 += hi_bf(u);
+    }
+    ws[(int64_t)blockIdx.x * cols + c] = s0;
+    ws[(int64_t)blockIdx.x * cols + c + 1] = s1;
+  }
+}
+
+__global__ void colsum_finish_kernel(const float* __restrict__ ws, int nb, int64_t cols,
+                                     bf16_t* __restrict__ out, int acc) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < nb; ++k) s += ws[(int64_t)k * cols + c];
+  if (acc) s += bf2f(out[c]);
+  out[c] = f2bf(s);
+}
+
+int colsum_blocks(int64_t rows, int64_t* chunk) {
+  int64_t nb = (rows + 63) / 64;
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  *chunk = (rows + nb - 1) / nb;
+  return (int)nb;
+}
+
+__global__ __launch_bounds__(256) void dropout_apply_kernel(const bf16_t* __restrict__ in,
+                                                            int64_t ldi, bf16_t* __restrict__ out,
+                                                            int64_t ldo, int64_t rows, int64_t cols,
+                                                            uint64_t seed, uint32_t thresh,
+                                                            float scale) {
+  const int64_t total = rows * cols;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / cols, c = e - r * cols;
+    const float v = bf2f(in[r * ldi + c]);
+    out[r * ldo + c] = f2bf(rng_keep(seed, (uint64_t)e, thresh) ? v * scale : 0.f);
+  }
+}
+
+__global__ __launch_bounds__(RED_NT) void gate_bwd_kernel(const bf16_t* __restrict__ dx,
+                                                          const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ gate,
+                                                          bf16_t* __restrict__ dy, int64_t n,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[RED_NT / 64];
+  const float t = tanhf(bf2f(*gate));
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * RED_NT + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * RED_NT) {
+    const float d = bf2f(dx[i]);
+    s += d * bf2f(y[i]);
+    dy[i] = f2bf(t * d);
+  }
+  s = block_sum<RED_NT>(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(RED_NT) void gate_finish_kernel(const float* __restrict__ partial,
+                                                             int nb, const bf16_t* __restrict__ gate,
+                                                             float* __restrict__ out) {
+  __shared__ float red[RED_NT / 64];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += RED_NT) s += partial[i];
+  s = block_sum<RED_NT>(s, red);
+  if (threadIdx.x == 0) {
+    const float t = tanhf(bf2f(*gate));
+    out[0] += s * (1.f - t * t);
+  }
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ in,
+                                                          bf16_t* __restrict__ out, int64_t n,
+                                                          int acc) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float v = in[i];
+    if (acc) v += bf2f(out[i]);
+    out[i] = f2bf(v);
+  }
+}
+
+int ew_blocks(int64_t n) {
+  int64_t nb = (n + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+}  // namespace
+
+extern "C" int64_t gvl_grad_norm_workspace_size(int64_t n) {
+  return (int64_t)red_blocks(n >> 3) * (int64_t)sizeof(float);
+}
+
+extern "C" int gvl_grad_norm(const void* g, int64_t n, float max_norm, void* workspace, float* out,
+                             gvl_stream_t stream) {
+  GVL_REQUIRE(g && workspace && out, "gvl_grad_norm: null buffer");
+  GVL_REQUIRE(gvl::aligned16(g), "gvl_grad_norm: g must be 16-byte aligned");
+  const int nb = red_blocks(n >> 3);
+  hipStream_t s = gvl::as_stream(stream);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(RED_NT), 0, s, static_cast<const bf16_t*>(g), n,
+                     static_cast<float*>(workspace));
+  GVL_LAUNCH_CHECK("gvl_grad_norm(sumsq)");
+  hipLaunchKernelGGL(norm_finish_kernel, dim3(1), dim3(RED_NT), 0, s,
+                     static_cast<const float*>(workspace), nb, max_norm, out);
+  GVL_LAUNCH_CHECK("gvl_grad_norm(finish)");
+  return 0;
+}
+
+extern "C" int gvl_adamw(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
+                         float lr, float beta1, float beta2, float eps, float weight_decay,
+                         int64_t step, const float* grad_scale, gvl_stream_t stream) {
+  GVL_REQUIRE(p && g && m && v, "gvl_adamw: null buffer");
+  GVL_REQUIRE(step >= 1, "gvl_adamw: step must be >= 1");
+  GVL_REQUIRE(gvl::aligned16(p) && gvl::aligned16(g) && gvl::aligned16(m) && gvl::aligned16(v),
+              "gvl_adamw: arenas must be 16-byte aligned");
+  if (n == 0) return 0;
+  AdamP a;
+  a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+  a.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(ew_blocks(n >> 3)), dim3(256), 0, gvl::as_stream(stream),
+                     static_cast<bf16_t*>(p), static_cast<const bf16_t*>(g),
+                     static_cast<bf16_t*>(m), static_cast<bf16_t*>(v), n, n_decay, a, grad_scale);
+  GVL_LAUNCH_CHECK("gvl_adamw");
+  return 0;
+}
+
+extern "C" int64_t gvl_colsum_workspace_size(int64_t rows, int64_t cols) {
+  int64_t chunk;
+  return (int64_t)colsum_blocks(rows, &chunk) * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
+                          int32_t accumulate, void* workspace, gvl_stream_t stream) {
+  GVL_REQUIRE(cols % 2 == 0 && ld % 2 == 0, "gvl_colsum: cols/ld must be even");
+  GVL_REQUIRE(workspace && out, "gvl_colsum: null buffer");
+  if (cols == 0) return 0;
+  int64_t chunk;
+  const int nb = colsum_blocks(rows, &chunk);
+  hipStream_t s = gvl::as_stream(stream);
+  if (rows == 0) {
+    hipMemsetAsync(workspace, 0, cols * sizeof(float), s);
+  } else {
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(x), rows, cols, ld, chunk,
+                       static_cast<float*>(workspace));
+    GVL_LAUNCH_CHECK("gvl_colsum(partial)");
+  }
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), rows == 0 ? 1 : nb, cols,
+                     static_cast<bf16_t*>(out), (int)accumulate);
+  GVL_LAUNCH_CHECK("gvl_colsum(finish)");
+  return 0;
+}
+
+extern "C" int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_out,
+                                      int64_t rows, int64_t cols, float p, uint64_t seed,
+                                      gvl_stream_t stream) {
+  GVL_REQUIRE(p >= 0.f && p < 1.f, "gvl_dropout_mask_apply: p out of range");
+  if (rows * cols == 0) return 0;
+  const uint32_t thresh = (uint32_t)((double)p * 4294967296.0);
+  hipLaunchKernelGGL(dropout_apply_kernel, dim3(ew_blocks(rows * cols)), dim3(256), 0,
+                     gvl::as_stream(stream), static_cast<const bf16_t*>(in), ld_in,
+                     static_cast<bf16_t*>(out), ld_out, rows, cols, seed, thresh, 1.f / (1.f - p));
+  GVL_LAUNCH_CHECK("gvl_dropout_mask_apply");
+  return 0;
+}
+
+extern "C" int64_t gvl_gate_bwd_workspace_size(int64_t n) {
+  return (int64_t)red_blocks(n) * (int64_t)sizeof(float);
+}
+
+extern "C" int gvl_gate_bwd(const void* dx, const void* y, const void* gate, void* dy,
+                            float* gate_grad, int64_t n, void* workspace, gvl_stream_t stream) {
+  GVL_REQUIRE(dx && y && gate && dy && gate_grad && workspace, "gvl_gate_bwd: null buffer");
+  const int nb = red_blocks(n);
+  hipStream_t s = gvl::as_stream(stream);
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(nb), dim3(RED_NT), 0, s, static_cast<const bf16_t*>(dx),
+                     static_cast<const bf16_t*>(y), static_cast<const bf16_t*>(gate),
+                     static_cast<bf16_t*>(dy), n, static_cast<float*>(workspace));
+  GVL_LAUNCH_CHECK("gvl_gate_bwd");
+  hipLaunchKernelGGL(gate_finish_kernel, dim3(1), dim3(RED_NT), 0, s,
+                     static_cast<const float*>(workspace), nb, static_cast<const bf16_t*>(gate),
+                     gate_grad);
+  GVL_LAUNCH_CHECK("gvl_gate_bwd(finish)");
+  return 0;
+}
+
+extern "C" int gvl_f32_to_bf16(const float* in, void* out, int64_t n, int32_t accumulate,
+                               gvl_stream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(ew_blocks(n)), dim3(256), 0, gvl::as_stream(stream),
+                     in, static_cast<bf16_t*>(out), n, (int)accumulate);
+  GVL_LAUNCH_CHECK("gvl_f32_to_bf16");
+  return 0;
+}

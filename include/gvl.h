@@ -1,0 +1,206 @@
+/*
+ * gvl.h — C-ABI of libgvl, the MI355X (gfx950) kernel library behind the
+ * gpt2-vision-language drop-in modules.
+ *
+ * The reference (theophile-lt/gpt2-vision-language) is pure Python/PyTorch: its
+ * operator boundary is the ATen op set its nn.Modules call.  Each
+ * entry point below replaces one or more of those ATen calls; the reference call
+ * site it stands in for is cited as file:line into /root/reference.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + int64 sizes/strides (in ELEMENTS), no torch types;
+ *   - bf16 tensors are raw 16-bit words; fp32 where stated;
+ *   - `stream` is a hipStream_t (the caller's torch.cuda.current_stream());
+ *   - return 0 on success, -1 on a rejected argument (shape/alignment),
+ *     -2 on a HIP launch error; gvl_last_error() returns the thread-local text;
+ *   - the library allocates nothing: every buffer and workspace is owned by the
+ *     caller (sizes from the *_workspace_size queries); no entry point
+ *     synchronises the device, so every call is capturable into a hipGraph.
+ */
+#ifndef GVL_H_
+#define GVL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GVL_ABI_VERSION 1
+
+typedef void* gvl_stream_t;
+
+const char* gvl_last_error(void);
+int gvl_abi_version(void);
+
+/* ------------------------------------------------------------------------- */
+/* GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulate, fused epilogue.
+ *   C[m][n] = epi( alpha * sum_k opA[m][k] * opB[k][n] )
+ *   opA: a_mn=0 -> A stored [M][K] (row stride lda);  a_mn=1 -> A stored [K][M].
+ *   opB: b_mn=0 -> B stored [N][K] (nn.Linear weight); b_mn=1 -> B stored [K][N].
+ * Epilogue order: *alpha_ptr, +bias[n], *dgelu(pre_in), {pre_out=v; v=gelu(v)},
+ *   dropout(p, seed, index m*N+n), *tanh(*gate), +residual, store (bf16 or fp32).
+ * Replaces: nn.Linear forward/backward (addmm/mm) at source/gpt2/train_gpt2.py:26-27,
+ *   50-58,96-97; gpt2_linear/model.py:125-129,172; gpt2_cross-att/model.py:39-41,81;
+ *   gpt2_q_former/model.py:119-130,151 and the gelu/dropout/residual adds around them. */
+typedef struct gvl_gemm_desc {
+  const void* a;
+  const void* b;
+  void* c;
+  int64_t m, n, k;
+  int64_t lda, ldb, ldc;
+  int32_t a_mn, b_mn;
+  float alpha;
+  const float* alpha_ptr; /* optional fp32 device scalar multiplied into alpha */
+  const void* bias;       /* optional bf16 [N] */
+  int32_t act;            /* 0 none, 1 gelu-tanh, 2 gelu-erf */
+  int32_t dact;           /* 0 none, 1 dgelu-tanh, 2 dgelu-erf (uses pre_in) */
+  void* pre_out;          /* optional bf16 [M][ldp]: value before activation */
+  const void* pre_in;     /* bf16 [M][ldp]: pre-activation for dact */
+  int64_t ldp;
+  const void* residual;   /* optional bf16 [M][ldr], may alias c */
+  int64_t ldr;
+  const void* gate;       /* optional bf16 scalar g: branch *= tanh(g) */
+  float drop_p;           /* dropout probability on the branch (0 = off) */
+  uint64_t seed;
+  int32_t c_fp32;         /* 1: C is fp32 */
+} gvl_gemm_desc;
+int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* LayerNorm over the last dim (eps given; reference uses 1e-5).
+ * Replaces nn.LayerNorm at source/gpt2/train_gpt2.py:66,68,94 (ln_1/ln_2/ln_f),
+ * gpt2_cross-att/model.py:91 (ln_x), gpt2_q_former/model.py:118-125. */
+int gvl_layernorm_fwd(const void* x, int64_t ldx, const void* w, const void* b,
+                      void* y, int64_t ldy, float* mean, float* rstd,
+                      int64_t rows, int64_t cols, float eps, gvl_stream_t stream);
+/* dx (bf16) = LN'(dy); if accumulate_dx, dx += result (residual-stream grad).
+ * dw/db (bf16, optional) get column sums; they need workspace
+ * gvl_layernorm_bwd_workspace_size(rows, cols) bytes. accumulate_wb adds into dw/db. */
+int64_t gvl_layernorm_bwd_workspace_size(int64_t rows, int64_t cols);
+int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                      const void* w, const float* mean, const float* rstd,
+                      void* dx, int64_t lddx, int32_t accumulate_dx,
+                      void* dw, void* db, int32_t accumulate_wb, void* workspace,
+                      int64_t rows, int64_t cols, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Fused attention, head dim 64, bf16 in/out, fp32 online softmax.
+ * q/k/v/o element (b,t,h,d) at ptr + b*s_b + t*s_t + h*s_h + d, so the packed
+ * c_attn output [B,T,3C] is consumed in place and o is written as [B,T,C]
+ * (the transpose(1,2).contiguous() of the reference is fused away).
+ * Replaces F.scaled_dot_product_attention at source/gpt2/train_gpt2.py:40 (causal),
+ * gpt2_cross-att/model.py:55 (non-causal bridge cross-attention) and the
+ * nn.MultiheadAttention core at gpt2_q_former/model.py:135,140 (attention-prob
+ * dropout p; need_weights output is discarded by the reference and not produced). */
+typedef struct gvl_attn_desc {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse; /* fp32 [B][H][Tq], natural-log row logsumexp of scale*q.k */
+  int64_t B, H, Tq, Tk;
+  int64_t q_sb, q_st, q_sh;
+  int64_t k_sb, k_st, k_sh;
+  int64_t v_sb, v_st, v_sh;
+  int64_t o_sb, o_st, o_sh;
+  int32_t causal;
+  float scale;
+  float drop_p;
+  uint64_t seed;
+} gvl_attn_desc;
+int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream);
+/* Backward: dO has the layout of o (do_* strides); dq/dk/dv the layouts of q/k/v
+ * (dq_*, dk_*, dv_* strides).  workspace: gvl_attn_bwd_workspace_size bytes. */
+typedef struct gvl_attn_bwd_desc {
+  const void* dout;
+  int64_t do_sb, do_st, do_sh;
+  void* dq;
+  int64_t dq_sb, dq_st, dq_sh;
+  void* dk;
+  int64_t dk_sb, dk_st, dk_sh;
+  void* dv;
+  int64_t dv_sb, dv_st, dv_sh;
+  void* workspace;
+} gvl_attn_bwd_desc;
+int64_t gvl_attn_bwd_workspace_size(const gvl_attn_desc* d);
+int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* g, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Row-wise cross-entropy over bf16 logits (fp32 math), fused softmax gradient.
+ * Logits row for target r: (r / rows_per_group) * group_stride + row_offset + r % rows_per_group
+ * (lets the caption loss read logits[:, M:M+T] in place).  targets int64 with
+ * ignore_index=-100; optional uint8 mask weights rows (cross-att masked mean).
+ * Writes row_loss[r] (fp32), dlogits[r] = softmax - onehot (bf16, unscaled, 0 for
+ * ignored rows, row stride ldd) and out[0]=mean loss, out[1]=1/count (count
+ * clamped to >=1 when mask_mode, torch 0/0 semantics otherwise).
+ * Replaces F.cross_entropy at source/gpt2/train_gpt2.py:124, gpt2_linear/model.py:206-210,
+ * gpt2_cross-att/model.py:170-185. */
+int gvl_cross_entropy(const void* logits, int64_t ldl, int64_t rows, int64_t vocab,
+                      int64_t rows_per_group, int64_t group_stride, int64_t row_offset,
+                      const int64_t* targets, const uint8_t* mask, int32_t mask_mode,
+                      float* row_loss, void* dlogits, int64_t ldd, float* out,
+                      gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Token + position embedding gather: out[row(r)] = wte[idx[r]] + wpe[r % T],
+ * row(r) = (r / T) * out_rows_per_seq + out_offset + r % T  (caption models write the
+ * text embeddings after the M image tokens).
+ * Replaces nn.Embedding x2 + add (+cat) at source/gpt2/train_gpt2.py:114-117,
+ * gpt2_linear/model.py:187-200, gpt2_cross-att/model.py:155-158. */
+int gvl_embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out,
+                      int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
+                      int64_t out_offset, gvl_stream_t stream);
+/* Backward: fp32 scatter-add into dwte_acc [V][C] and dwpe_acc [T][C] (caller zeroes). */
+int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc, float* dwpe_acc,
+                      int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
+                      int64_t out_offset, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* CLIP token pooling: [CLS] + adaptive_avg_pool2d(side x side -> 4 x 8) + L2 normalise
+ * (eps 1e-12).  in: [B][1+side*side][D] (fp32 or bf16), out: [B][33][D] (fp32 or bf16).
+ * Replaces pool_clip_197_to_33_avg_with_cls, gpt2_linear/model.py:240-254. */
+int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
+                  int64_t B, int64_t L, int64_t D, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Optimizer path over flat bf16 arenas (params / grads / exp_avg / exp_avg_sq).
+ * gvl_grad_norm: out[0] = ||g||_2 (fp32), out[1] = clip coefficient
+ *   min(1, max_norm / (norm + 1e-6)) — torch.nn.utils.clip_grad_norm_ at
+ *   source/gpt2/train_gpt2.py:472.  workspace: gvl_grad_norm_workspace_size(n).
+ * gvl_adamw: decoupled weight decay on elements [0, n_decay), none after; grads are
+ *   multiplied by *grad_scale (the clip coefficient) on the fly; bias corrections use
+ *   `step` (1-based) — torch.optim.AdamW(fused=True) at train_gpt2.py:140-143, :476. */
+int64_t gvl_grad_norm_workspace_size(int64_t n);
+int gvl_grad_norm(const void* g, int64_t n, float max_norm, void* workspace, float* out,
+                  gvl_stream_t stream);
+int gvl_adamw(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
+              float lr, float beta1, float beta2, float eps, float weight_decay,
+              int64_t step, const float* grad_scale, gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
+/* Small fused elementwise helpers on the hot path. */
+/* Column sums of a bf16 [rows][cols] matrix (row stride ld) -> bf16 out[cols]
+ * (bias gradients); accumulate adds into out. workspace: gvl_colsum_workspace_size. */
+int64_t gvl_colsum_workspace_size(int64_t rows, int64_t cols);
+int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
+               int32_t accumulate, void* workspace, gvl_stream_t stream);
+/* out[r][c] = in[r][c] * keep(seed, r*cols+c) / (1-p) — dropout backward, with the
+ * same counter-based mask the GEMM epilogue applies. */
+int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_out,
+                           int64_t rows, int64_t cols, float p, uint64_t seed,
+                           gvl_stream_t stream);
+/* out[i] = tanh(*gate) * in[i] and gate_grad (fp32 scalar, accumulated) +=
+ * (1 - tanh^2) * sum_i in[i] * y[i] — backward of x + tanh(g) * y
+ * (gpt2_cross-att/model.py:101). */
+int gvl_gate_bwd(const void* dx, const void* y, const void* gate, void* dy, float* gate_grad,
+                 int64_t n, void* workspace, gvl_stream_t stream);
+int64_t gvl_gate_bwd_workspace_size(int64_t n);
+/* fp32 -> bf16 conversion with optional accumulate into the bf16 destination. */
+int gvl_f32_to_bf16(const float* in, void* out, int64_t n, int32_t accumulate,
+                    gvl_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GVL_H_ */
