@@ -1,0 +1,530 @@
+// Fused attention for head dim 64 on gfx950 MFMA (16x16x32 bf16), forward + backward.
+//
+// Forward (flash-style, online softmax in fp32): block = (64-query tile, head, batch),
+// 4 waves x 16 query rows.  K and V tiles of 64 keys are register-staged into a
+// double-buffered LDS ring.  S is computed "swapped" (K fragment as the MFMA A operand),
+// which leaves one query row per lane (lane&15) and 16 keys in registers, so the row
+// max/sum need only two cross-lane steps, and the P fragment of the following P.V MFMA is
+// lane-local (the MFMA k-slots are permuted to match; V is read with ds_read_b64_tr_b16).
+// The output accumulator keeps the same query on the lane, so rescales are lane-local.
+//
+// Backward (FA2 recompute, no atomics, deterministic): a preprocess kernel computes
+// D = rowsum(dO*O); dQ is produced by a query-tile kernel looping over key tiles and
+// dK/dV by a key-tile kernel looping over query tiles.  P is recomputed from the saved
+// log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash mask on (b,h,q,k), identical in
+// every kernel.
+#include "common.h"
+#include "capi_util.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+constexpr int D = 64;        // head dim
+constexpr int QT = 64;       // query tile per block
+constexpr int KT = 64;       // key tile
+constexpr int NT = 256;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct AttnP {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o; float* lse;
+  int64_t B, H, Tq, Tk;
+  int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
+  int causal;
+  float scale;       // softmax scale (1/sqrt(64))
+  float c2;          // scale * log2(e)
+  int has_drop;
+  uint32_t drop_thresh;
+  float drop_scale;
+  uint64_t seed;
+};
+
+struct AttnG {
+  const bf16_t* dout; int64_t do_sb, do_st, do_sh;
+  bf16_t* dq; int64_t dq_sb, dq_st, dq_sh;
+  bf16_t* dk; int64_t dk_sb, dk_st, dk_sh;
+  bf16_t* dv; int64_t dv_sb, dv_st, dv_sh;
+  float* Dws;
+};
+
+// [64 rows][64 d] bf16 tile, 128-B rows.  Row image for ds_read_b128 fragments.
+GVL_DEV int swz_row(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// Image for ds_read_b64_tr_b16-only tiles (V in the forward): conflict-free transposed reads.
+GVL_DEV int swz_tr(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
+
+// Register-stage a 64x64 tile (rows r0.., valid rows < R) from a strided tensor.
+GVL_DEV void load_rows(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t r0, int64_t R, int tid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    if (r0 + row < R) r[it] = *reinterpret_cast<const uint4*>(base + (r0 + row) * st + ch * 8);
+    else r[it] = make_uint4(0, 0, 0, 0);
+  }
+}
+template <bool TR>
+GVL_DEV void store_rows(const uint4 (&r)[2], char* lds, int tid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    const int off = TR ? swz_tr(row, ch) : swz_row(row, ch);
+    *reinterpret_cast<uint4*>(lds + off) = r[it];
+  }
+}
+
+// Row fragment (16 rows from row0, k-step s over d): lane holds tile[row0+(l&15)][32s+8G..+7].
+GVL_DEV short8_t frag_row(const char* lds, int row0, int s, int lane) {
+  const int row = row0 + (lane & 15), ch = 4 * s + (lane >> 4);
+  return *reinterpret_cast<const short8_t*>(lds + swz_row(row, ch));
+}
+// Transposed fragment for the permuted k-slot order used by P.V-type products:
+// lane (G, i) gets column 16t+i of rows {32s+4G+0..3} (elements 0..3) and
+// {32s+16+4G+0..3} (elements 4..7).
+template <bool TR>
+GVL_DEV short8_t frag_tr(const char* lds, int t, int s, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = 2 * t + (p >> 1);
+  const int ra = 32 * s + 4 * G + q, rb = ra + 16;
+  const int oa = (TR ? swz_tr(ra, ch) : swz_row(ra, ch)) + (p & 1) * 8;
+  const int ob = (TR ? swz_tr(rb, ch) : swz_row(rb, ch)) + (p & 1) * 8;
+  short8_t r;
+  r.lo = lds_read_tr(lds + oa);
+  r.hi = lds_read_tr(lds + ob);
+  return r;
+}
+
+GVL_DEV short8_t load_frag_global(const bf16_t* rowptr, int s, int lane, bool ok) {
+  if (!ok) return short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint4 u = *reinterpret_cast<const uint4*>(rowptr + 32 * s + 8 * (lane >> 4));
+  return __builtin_bit_cast(short8_t, u);
+}
+
+GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
+  uint4 u = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3]));
+  return __builtin_bit_cast(short8_t, u);
+}
+
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4;
+  const int64_t b = blockIdx.z, h = blockIdx.y;
+  const int64_t qblk0 = (int64_t)blockIdx.x * QT;
+  const int64_t q = qblk0 + wave * 16 + (lane & 15);
+  const bool qok = q < p.Tq;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+
+  short8_t qf[2];
+  qf[0] = load_frag_global(qbase + q * p.q_st, 0, lane, qok);
+  qf[1] = load_frag_global(qbase + q * p.q_st, 1, lane, qok);
+
+  int64_t kend = p.Tk;
+  if (p.causal) {
+    const int64_t lim = qblk0 + QT;
+    if (lim < kend) kend = lim;
+  }
+  const int nkt = (int)((kend + KT - 1) / KT);
+
+  float4_t o[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) o[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q) * (uint64_t)p.Tk;
+
+  uint4 rk[2], rv[2];
+  load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
+  load_rows(rv, vbase, p.v_st, 0, p.Tk, tid);
+  store_rows<false>(rk, smem[0][0], tid);
+  store_rows<true>(rv, smem[0][1], tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+    }
+    const char* ks = smem[kt & 1][0];
+    const char* vs = smem[kt & 1][1];
+    const int64_t k0 = (int64_t)kt * KT;
+    float4_t sc[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) sc[n] = mfma16(frag_row(ks, 16 * n, s, lane), qf[s], sc[n]);
+    }
+    // scale + mask; lane holds S[q][key = k0 + 16n + 4G + r]
+    float mx = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t key = k0 + 16 * n + 4 * G + r;
+        float sv = sc[n][r] * p.c2;
+        if (key >= p.Tk || (p.causal && key > q)) sv = -INFINITY;
+        sc[n][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = exp2f(m - msub);
+    m = mnew;
+    float ls = 0.f;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(sc[n][r] - msub);
+        ls += e;
+        float pe = e;
+        if (p.has_drop) {
+          const int64_t key = k0 + 16 * n + 4 * G + r;
+          pe = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
+        }
+        sc[n][r] = pe;
+      }
+    l = l * alpha + ls;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] *= alpha;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const short8_t pf = pack_frag(sc[2 * s], sc[2 * s + 1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = mfma16(frag_tr<true>(vs, t, s, lane), pf, o[t]);
+    }
+    if (more) {
+      store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
+      store_rows<true>(rv, smem[(kt + 1) & 1][1], tid);
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qok) return;
+  const float inv = 1.f / l;
+  bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q * p.o_st;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int d = 16 * t + 4 * G;
+    *reinterpret_cast<uint2*>(orow + d) =
+        make_uint2(pack2(o[t][0] * inv, o[t][1] * inv), pack2(o[t][2] * inv, o[t][3] * inv));
+  }
+  if (G == 0 && p.lse) p.lse[(b * p.H + h) * p.Tq + q] = (m + log2f(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------------
+// D[b,h,q] = sum_d dO*O  (one thread per row, 8 x 16-B loads each)
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = p.B * p.H * p.Tq;
+  if (idx >= total) return;
+  const int64_t q = idx % p.Tq, bh = idx / p.Tq, h = bh % p.H, b = bh / p.H;
+  const bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q * p.o_st;
+  const bf16_t* drow = g.dout + b * g.do_sb + h * g.do_sh + q * g.do_st;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const uint4 a = *reinterpret_cast<const uint4*>(orow + c * 8);
+    const uint4 d = *reinterpret_cast<const uint4*>(drow + c * 8);
+    s += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
+         hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
+         lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
+  }
+  g.Dws[idx] = s;
+}
+
+// dQ: block = (64-query tile, head, batch), waves own 16 query rows each.
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG g) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4;
+  const int64_t b = blockIdx.z, h = blockIdx.y;
+  const int64_t qblk0 = (int64_t)blockIdx.x * QT;
+  const int64_t q = qblk0 + wave * 16 + (lane & 15);
+  const bool qok = q < p.Tq;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dobase = g.dout + b * g.do_sb + h * g.do_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  short8_t qf[2], df[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    qf[s] = load_frag_global(qbase + q * p.q_st, s, lane, qok);
+    df[s] = load_frag_global(dobase + q * g.do_st, s, lane, qok);
+  }
+  const int64_t ridx = (b * p.H + h) * p.Tq + q;
+  const float lse2 = qok ? p.lse[ridx] * LOG2E : 0.f;
+  const float Dq = qok ? g.Dws[ridx] : 0.f;
+  const uint64_t drow = (uint64_t)ridx * (uint64_t)p.Tk;
+
+  int64_t kend = p.Tk;
+  if (p.causal) {
+    const int64_t lim = qblk0 + QT;
+    if (lim < kend) kend = lim;
+  }
+  const int nkt = (int)((kend + KT - 1) / KT);
+  float4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 rk[2], rv[2];
+  load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
+  load_rows(rv, vbase, p.v_st, 0, p.Tk, tid);
+  store_rows<false>(rk, smem[0][0], tid);
+  store_rows<false>(rv, smem[0][1], tid);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+    }
+    const char* ks = smem[kt & 1][0];
+    const char* vs = smem[kt & 1][1];
+    const int64_t k0 = (int64_t)kt * KT;
+    float4_t sc[4], dp[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+      dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sc[n] = mfma16(frag_row(ks, 16 * n, s, lane), qf[s], sc[n]);
+        dp[n] = mfma16(frag_row(vs, 16 * n, s, lane), df[s], dp[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t key = k0 + 16 * n + 4 * G + r;
+        const bool ok = qok && key < p.Tk && !(p.causal && key > q);
+        const float pv = ok ? exp2f(sc[n][r] * p.c2 - lse2) : 0.f;
+        float dpv = dp[n][r];
+        if (p.has_drop)
+          dpv = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? dpv * p.drop_scale : 0.f;
+        sc[n][r] = pv * (dpv - Dq);  // dS
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const short8_t sf = pack_frag(sc[2 * s], sc[2 * s + 1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma16(frag_tr<false>(ks, t, s, lane), sf, acc[t]);
+    }
+    if (more) {
+      store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
+      store_rows<false>(rv, smem[(kt + 1) & 1][1], tid);
+    }
+    __syncthreads();
+  }
+  if (!qok) return;
+  bf16_t* dst = g.dq + b * g.dq_sb + h * g.dq_sh + q * g.dq_st;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int d = 16 * t + 4 * G;
+    *reinterpret_cast<uint2*>(dst + d) =
+        make_uint2(pack2(acc[t][0] * p.scale, acc[t][1] * p.scale),
+                   pack2(acc[t][2] * p.scale, acc[t][3] * p.scale));
+  }
+}
+
+// dK/dV: block = (64-key tile, head, batch), waves own 16 keys each; loop over query tiles.
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG g) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][QT * D * 2];  // [stage][Q,dO]
+  __shared__ float sl[2][2][QT];                                       // [stage][lse2, D]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4;
+  const int64_t b = blockIdx.z, h = blockIdx.y;
+  const int64_t kblk0 = (int64_t)blockIdx.x * KT;
+  const int64_t key = kblk0 + wave * 16 + (lane & 15);
+  const bool kok = key < p.Tk;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dobase = g.dout + b * g.do_sb + h * g.do_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  const int64_t rbase = (b * p.H + h) * p.Tq;
+  short8_t kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kf[s] = load_frag_global(kbase + key * p.k_st, s, lane, kok);
+    vf[s] = load_frag_global(vbase + key * p.v_st, s, lane, kok);
+  }
+  const int qt_first = p.causal ? (int)(kblk0 / QT) : 0;
+  const int nqt = (int)((p.Tq + QT - 1) / QT);
+  float4_t dk[4], dv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  if (qt_first < nqt) {
+    uint4 rq[2], rd[2];
+    float rl = 0.f, rD = 0.f;
+    auto fetch = [&](int qt) {
+      const int64_t q0 = (int64_t)qt * QT;
+      load_rows(rq, qbase, p.q_st, q0, p.Tq, tid);
+      load_rows(rd, dobase, g.do_st, q0, p.Tq, tid);
+      if (tid < QT) {
+        const int64_t qq = q0 + tid;
+        rl = qq < p.Tq ? p.lse[rbase + qq] * LOG2E : 0.f;
+        rD = qq < p.Tq ? g.Dws[rbase + qq] : 0.f;
+      }
+    };
+    auto put = [&](int st) {
+      store_rows<false>(rq, smem[st][0], tid);
+      store_rows<false>(rd, smem[st][1], tid);
+      if (tid < QT) {
+        sl[st][0][tid] = rl;
+        sl[st][1][tid] = rD;
+      }
+    };
+    fetch(qt_first);
+    put(0);
+    __syncthreads();
+    for (int qt = qt_first; qt < nqt; ++qt) {
+      const int st = (qt - qt_first) & 1;
+      const bool more = qt + 1 < nqt;
+      if (more) fetch(qt + 1);
+      const char* qs = smem[st][0];
+      const char* ds = smem[st][1];
+      const int64_t q0 = (int64_t)qt * QT;
+      float4_t sc[4], dp[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+        dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          sc[n] = mfma16(frag_row(qs, 16 * n, s, lane), kf[s], sc[n]);
+          dp[n] = mfma16(frag_row(ds, 16 * n, s, lane), vf[s], dp[n]);
+        }
+      }
+      // lane holds S[q = q0 + 16n + 4G + r][key]
+      float4_t pd[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * n + 4 * G + r;
+          const int64_t qq = q0 + qi;
+          const bool ok = kok && qq < p.Tq && !(p.causal && key > qq);
+          const float pv = ok ? exp2f(sc[n][r] * p.c2 - sl[st][0][qi]) : 0.f;
+          float pdrop = pv, dpv = dp[n][r];
+          if (p.has_drop) {
+            const bool keep =
+                rng_keep(p.seed, (uint64_t)(rbase + qq) * (uint64_t)p.Tk + (uint64_t)key, p.drop_thresh);
+            pdrop = keep ? pv * p.drop_scale : 0.f;
+            dpv = keep ? dpv * p.drop_scale : 0.f;
+          }
+          pd[n][r] = pdrop;
+          sc[n][r] = pv * (dpv - sl[st][1][qi]);  // dS
+        }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const short8_t pf = pack_frag(pd[2 * s], pd[2 * s + 1]);
+        const short8_t sf = pack_frag(sc[2 * s], sc[2 * s + 1]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          dv[t] = mfma16(frag_tr<false>(ds, t, s, lane), pf, dv[t]);
+          dk[t] = mfma16(frag_tr<false>(qs, t, s, lane), sf, dk[t]);
+        }
+      }
+      if (more) put(st ^ 1);  // stage st^1 was last read in iteration qt-1
+      __syncthreads();
+    }
+  }
+  if (!kok) return;
+  bf16_t* dkr = g.dk + b * g.dk_sb + h * g.dk_sh + key * g.dk_st;
+  bf16_t* dvr = g.dv + b * g.dv_sb + h * g.dv_sh + key * g.dv_st;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int d = 16 * t + 4 * G;
+    *reinterpret_cast<uint2*>(dkr + d) =
+        make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale), pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
+    *reinterpret_cast<uint2*>(dvr + d) =
+        make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+  }
+}
+
+int fill(const gvl_attn_desc* d, AttnP& p) {
+  GVL_REQUIRE(d && d->q && d->k && d->v && d->o, "gvl_attn: null tensor");
+  GVL_REQUIRE(d->B > 0 && d->H > 0 && d->Tq > 0 && d->Tk > 0, "gvl_attn: empty shape");
+  GVL_REQUIRE(d->B <= 65535 && d->H <= 65535, "gvl_attn: B/H too large");
+  const int64_t st[] = {d->q_sb, d->q_st, d->q_sh, d->k_sb, d->k_st, d->k_sh,
+                        d->v_sb, d->v_st, d->v_sh, d->o_sb, d->o_st, d->o_sh};
+  for (int64_t s : st) GVL_REQUIRE(s % 8 == 0, "gvl_attn: strides must be multiples of 8 elements");
+  GVL_REQUIRE(gvl::aligned16(d->q) && gvl::aligned16(d->k) && gvl::aligned16(d->v) &&
+                  gvl::aligned16(d->o),
+              "gvl_attn: tensors must be 16-byte aligned");
+  GVL_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "gvl_attn: drop_p out of range");
+  p.q = static_cast<const bf16_t*>(d->q);
+  p.k = static_cast<const bf16_t*>(d->k);
+  p.v = static_cast<const bf16_t*>(d->v);
+  p.o = static_cast<bf16_t*>(d->o);
+  p.lse = d->lse;
+  p.B = d->B; p.H = d->H; p.Tq = d->Tq; p.Tk = d->Tk;
+  p.q_sb = d->q_sb; p.q_st = d->q_st; p.q_sh = d->q_sh;
+  p.k_sb = d->k_sb; p.k_st = d->k_st; p.k_sh = d->k_sh;
+  p.v_sb = d->v_sb; p.v_st = d->v_st; p.v_sh = d->v_sh;
+  p.o_sb = d->o_sb; p.o_st = d->o_st; p.o_sh = d->o_sh;
+  p.causal = d->causal;
+  p.scale = d->scale;
+  p.c2 = d->scale * LOG2E;
+  p.has_drop = d->drop_p > 0.f;
+  p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
+  p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
+  p.seed = d->seed;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
+  AttnP p;
+  if (fill(d, p)) return -1;
+  dim3 grid((unsigned)((d->Tq + QT - 1) / QT), (unsigned)d->H, (unsigned)d->B);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(NT), 0, gvl::as_stream(stream), p);
+  GVL_LAUNCH_CHECK("gvl_attn_fwd");
+  return 0;
+}
+
+extern "C" int64_t gvl_attn_bwd_workspace_size(const gvl_attn_desc* d) {
+  return d->B * d->H * d->Tq * (int64_t)sizeof(float);
+}
+
+extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
+                            gvl_stream_t stream) {
+  AttnP p;
+  if (fill(d, p)) return -1;
+  GVL_REQUIRE(gd && gd->dout && gd->dq && gd->dk && gd->dv && gd->workspace && d->lse,
+              "gvl_attn_bwd: null tensor");
+  const int64_t st[] = {gd->do_sb, gd->do_st, gd->do_sh, gd->dq_sb, gd->dq_st, gd->dq_sh,
+                        gd->dk_sb, gd->dk_st, gd->dk_sh, gd->dv_sb, gd->dv_st, gd->dv_sh};
+  for (int64_t s : st) GVL_REQUIRE(s % 8 == 0, "gvl_attn_bwd: strides must be multiples of 8");
+  AttnG g;
+  g.dout = static_cast<const bf16_t*>(gd->dout);
+  g.do_sb = gd->do_sb; g.do_st = gd->do_st; g.do_sh = gd->do_sh;
+  g.dq = static_cast<bf16_t*>(gd->dq);
+  g.dq_sb = gd->dq_sb; g.dq_st = gd->dq_st; g.dq_sh = gd->dq_sh;
+  g.dk = static_cast<bf16_t*>(gd->dk);
+  g.dk_sb = gd->dk_sb; g.dk_st = gd->dk_st; g.dk_sh = gd->dk_sh;
+  g.dv = static_cast<bf16_t*>(gd->dv);
+  g.dv_sb = gd->dv_sb; g.dv_st = gd->dv_st; g.dv_sh = gd->dv_sh;
+  g.Dws = static_cast<float*>(gd->workspace);
+  hipStream_t s = gvl::as_stream(stream);
+  const int64_t rows = d->B * d->H * d->Tq;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
+  GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
+  dim3 gq((unsigned)((d->Tq + QT - 1) / QT), (unsigned)d->H, (unsigned)d->B);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(NT), 0, s, p, g);
+  GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
+  dim3 gk((unsigned)((d->Tk + KT - 1) / KT), (unsigned)d->H, (unsigned)d->B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, gk, dim3(NT), 0, s, p, g);
+  GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");
+  return 0;
+}

@@ -89,11 +89,12 @@ __global__ __launch_bounds__(1024) void ce_finalize_kernel(const float* __restri
   __shared__ float red[16];
   float s = 0.f, n = 0.f;
   for (int64_t r = threadIdx.x; r < rows; r += 1024) {
-    const bool valid = (targets[r] != -100) && (mask == nullptr || mask[r] != 0);
-    if (valid) {
-      s += row_loss[r];
-      n += 1.f;
-    }
+    const bool mk = (mask == nullptr || mask[r] != 0);
+    const bool valid = (targets[r] != -100) && mk;
+    if (valid) s += row_loss[r];
+    // masked mean divides by sum(mask) (gpt2_cross-att/model.py:184-185); the ignore_index
+    // mean by the number of non-ignored targets (F.cross_entropy default)
+    if (mask_mode ? mk : valid) n += 1.f;
   }
   s = block_sum<1024>(s, red);
   n = block_sum<1024>(n, red);

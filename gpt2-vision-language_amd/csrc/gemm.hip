@@ -202,6 +202,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
           v[r] = rng_keep(p.seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
       }
       if (p.gate) {
+        if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient
+          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= gatev;
       }

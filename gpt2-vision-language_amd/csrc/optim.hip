@@ -262,7 +262,7 @@ extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld,
   const int nb = colsum_blocks(rows, &chunk);
   hipStream_t s = gvl::as_stream(stream);
   if (rows == 0) {
-    hipMemsetAsync(workspace, 0, cols * sizeof(float), s);
+    (void)hipMemsetAsync(workspace, 0, cols * sizeof(float), s);
   } else {
     hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s,
                        static_cast<const bf16_t*>(x), rows, cols, ld, chunk,

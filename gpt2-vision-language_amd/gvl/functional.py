@@ -1,0 +1,474 @@
+"""Autograd Functions over the libgvl kernels — the fused units the drop-in modules call.
+
+Granularity follows the MI355X design: one Function per GPT-2 block (so
+DDP-style gradient buckets become ready block by block during backward), fused
+MHA / MLP / gated cross-attention units for the bridges, and a fused lm_head +
+cross-entropy.  Frozen parameters (requires_grad=False, the caption setting) skip their
+weight-gradient GEMMs entirely via ctx.needs_input_grad.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+ATT_SCALE = 1.0 / math.sqrt(64.0)
+
+
+def bf(t):
+    """Parameters are bf16 on the GPU path (the reference runs model.to(bfloat16));
+    fp32 parameters are cast per call, as autocast would."""
+    if t is None:
+        return None
+    return t if t.dtype == BF16 else t.to(BF16)
+
+
+def new_seed():
+    return int(torch.randint(1, 2**62, (1,)).item())
+
+
+def _need(ctx, i):
+    return ctx.needs_input_grad[i]
+
+
+# ------------------------------------------------------------------------ GPT-2 block
+class GPTBlockFn(torch.autograd.Function):
+    """x + attn(ln_1 x); then + mlp(ln_2 .) — source/gpt2/train_gpt2.py:62-74.
+
+    Forward: LN -> c_attn GEMM(+bias) -> causal attention straight out of the packed qkv
+    -> c_proj GEMM(+bias, +residual) -> LN -> c_fc GEMM(+bias, GELU-tanh, saves the
+    pre-activation) -> c_proj GEMM(+bias, +residual).
+    """
+
+    @staticmethod
+    def forward(ctx, x, ln1_w, ln1_b, attn_w, attn_b, aproj_w, aproj_b, ln2_w, ln2_b, fc_w,
+                fc_b, mproj_w, mproj_b, n_head: int, causal: bool = True):
+        B, T, C = x.shape
+        x2 = x.reshape(B * T, C)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        xn1, m1, r1 = K.layernorm_fwd(x2, ln1_w, ln1_b)
+        qkv = K.linear(xn1, attn_w, attn_b)
+        q3 = qkv.view(B, T, 3 * C)
+        y, lse = K.attn_fwd(q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], n_head, causal)
+        y2 = y.view(B * T, C)
+        xm = K.linear(y2, aproj_w, aproj_b, residual=x2)
+        xn2, m2, r2 = K.layernorm_fwd(xm, ln2_w, ln2_b)
+        hpre = torch.empty(B * T, fc_w.shape[0], dtype=BF16, device=x.device)
+        h = K.linear(xn2, fc_w, fc_b, act=1, pre_out=hpre)
+        out = K.linear(h, mproj_w, mproj_b, residual=xm)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(x2, xn1, m1, r1, qkv, y, lse, xm, xn2, m2, r2, hpre, h, ln1_w,
+                                  attn_w, aproj_w, ln2_w, fc_w, mproj_w)
+            ctx.shape = (B, T, C, n_head, causal)
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, xn1, m1, r1, qkv, y, lse, xm, xn2, m2, r2, hpre, h, ln1_w, attn_w, aproj_w, ln2_w,
+         fc_w, mproj_w) = ctx.saved_tensors
+        B, T, C, H, causal = ctx.shape
+        g = [None] * 15
+        d2 = dout.reshape(B * T, C)
+        if d2.dtype != BF16:
+            d2 = d2.to(BF16)
+        d2 = d2.contiguous()
+        # MLP c_proj
+        if _need(ctx, 11):
+            g[11] = K.linear_dw(d2, h)
+        if _need(ctx, 12):
+            g[12] = K.colsum(d2)
+        dpre = K.linear_dx(d2, mproj_w, dact=1, pre_in=hpre)
+        if _need(ctx, 9):
+            g[9] = K.linear_dw(dpre, xn2)
+        if _need(ctx, 10):
+            g[10] = K.colsum(dpre)
+        dxn2 = K.linear_dx(dpre, fc_w)
+        dxm = d2.clone()
+        dw2 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 7) else None
+        db2 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 8) else None
+        K.layernorm_bwd(dxn2, xm, ln2_w, m2, r2, dx=dxm, accumulate_dx=True, dw=dw2, db=db2)
+        g[7], g[8] = dw2, db2
+        # attention c_proj
+        if _need(ctx, 5):
+            g[5] = K.linear_dw(dxm, y.view(B * T, C))
+        if _need(ctx, 6):
+            g[6] = K.colsum(dxm)
+        dy = K.linear_dx(dxm, aproj_w)
+        dqkv = torch.empty(B * T, 3 * C, dtype=BF16, device=d2.device)
+        q3 = qkv.view(B, T, 3 * C)
+        dq3 = dqkv.view(B, T, 3 * C)
+        K.attn_bwd(dy.view(B, T, C), q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], y, lse, H,
+                   causal, dq3[:, :, :C], dq3[:, :, C:2 * C], dq3[:, :, 2 * C:])
+        if _need(ctx, 3):
+            g[3] = K.linear_dw(dqkv, xn1)
+        if _need(ctx, 4):
+            g[4] = K.colsum(dqkv)
+        dxn1 = K.linear_dx(dqkv, attn_w)
+        dw1 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 1) else None
+        db1 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 2) else None
+        K.layernorm_bwd(dxn1, x2, ln1_w, m1, r1, dx=dxm, accumulate_dx=True, dw=dw1, db=db1)
+        g[1], g[2] = dw1, db1
+        g[0] = dxm.view(B, T, C) if _need(ctx, 0) else None
+        return tuple(g)
+
+
+# ------------------------------------------------------------------------- LayerNorm
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float = 1e-5):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if x2.dtype != BF16:
+            x2 = x2.to(BF16)
+        x2 = x2.contiguous()
+        y, mean, rstd = K.layernorm_fwd(x2, w, b, eps)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(x2, w, mean, rstd)
+            ctx.shp = shp
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        C = x2.shape[1]
+        d2 = dy.reshape(-1, C).to(BF16).contiguous()
+        dw = torch.empty(C, dtype=BF16, device=x2.device) if _need(ctx, 1) else None
+        db = torch.empty(C, dtype=BF16, device=x2.device) if _need(ctx, 2) else None
+        dx = None
+        if _need(ctx, 0) or dw is not None or db is not None:
+            dx = K.layernorm_bwd(d2, x2, w, mean, rstd, dw=dw, db=db)
+        return (dx.view(ctx.shp) if (dx is not None and _need(ctx, 0)) else None), dw, db, None
+
+
+# ---------------------------------------------------------------------------- Linear
+class LinearFn(torch.autograd.Function):
+    """y = [residual +] [tanh(gate) *] dropout(x W^T + b)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, residual=None, gate=None, drop_p: float = 0.0, seed: int = 0):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if x2.dtype != BF16:
+            x2 = x2.to(BF16)
+        x2 = x2.contiguous()
+        N = w.shape[0]
+        r2 = None
+        if residual is not None:
+            r2 = residual.reshape(-1, N)
+            if r2.dtype != BF16:
+                r2 = r2.to(BF16)
+            r2 = r2.contiguous()
+        ybr = None
+        if gate is not None:
+            ybr = torch.empty(x2.shape[0], N, dtype=BF16, device=x.device)
+        y = K.linear(x2, w, b, residual=r2, gate=gate, pre_out=ybr, drop_p=drop_p, seed=seed)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(x2, w, gate, ybr)
+            ctx.cfg = (shp, N, drop_p, seed, residual is not None)
+        return y.view(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, gate, ybr = ctx.saved_tensors
+        shp, N, drop_p, seed, has_res = ctx.cfg
+        d2 = dy.reshape(-1, N)
+        if d2.dtype != BF16:
+            d2 = d2.to(BF16)
+        d2 = d2.contiguous()
+        dres = dy if (has_res and _need(ctx, 3)) else None
+        dgate = None
+        dbr = d2
+        if gate is not None:
+            gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
+            dbr = K.gate_bwd(d2, ybr, gate, gacc)
+            if _need(ctx, 4):
+                dgate = gacc.to(gate.dtype).view_as(gate)
+        if drop_p > 0:
+            dbr = K.dropout_mask_apply(dbr, drop_p, seed)
+        dx = K.linear_dx(dbr, w).view(shp) if _need(ctx, 0) else None
+        dw = K.linear_dw(dbr, x2) if _need(ctx, 1) else None
+        db = K.colsum(dbr) if _need(ctx, 2) else None
+        return dx, dw, db, dres, dgate, None, None
+
+
+class MLPFn(torch.autograd.Function):
+    """y = [residual +] dropout(act(x W1^T + b1) W2^T + b2); act: 1 gelu-tanh, 2 gelu-erf."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual=None, act: int = 1, drop_p: float = 0.0,
+                seed: int = 0):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(BF16).contiguous()
+        hpre = torch.empty(x2.shape[0], w1.shape[0], dtype=BF16, device=x.device)
+        h = K.linear(x2, w1, b1, act=act, pre_out=hpre)
+        r2 = residual.reshape(-1, w2.shape[0]).to(BF16).contiguous() if residual is not None else None
+        y = K.linear(h, w2, b2, residual=r2, drop_p=drop_p, seed=seed)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(x2, w1, w2, hpre, h)
+            ctx.cfg = (shp, act, drop_p, seed, residual is not None)
+        return y.view(*shp[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, w2, hpre, h = ctx.saved_tensors
+        shp, act, drop_p, seed, has_res = ctx.cfg
+        d2 = dy.reshape(-1, w2.shape[0]).to(BF16).contiguous()
+        dres = dy if (has_res and _need(ctx, 5)) else None
+        if drop_p > 0:
+            d2 = K.dropout_mask_apply(d2, drop_p, seed)
+        dw2 = K.linear_dw(d2, h) if _need(ctx, 3) else None
+        db2 = K.colsum(d2) if _need(ctx, 4) else None
+        dpre = K.linear_dx(d2, w2, dact=act, pre_in=hpre)
+        dw1 = K.linear_dw(dpre, x2) if _need(ctx, 1) else None
+        db1 = K.colsum(dpre) if _need(ctx, 2) else None
+        dx = K.linear_dx(dpre, w1).view(shp) if _need(ctx, 0) else None
+        return dx, dw1, db1, dw2, db2, dres, None, None, None
+
+
+# ------------------------------------------------------------------ attention units
+class MHAFn(torch.autograd.Function):
+    """nn.MultiheadAttention(batch_first) core + out_proj + dropout + residual
+    (gpt2_q_former/model.py:119-141): out = residual + drop(out_proj(attn(...))).
+
+    self_attn: q_in is also the key/value input and the packed in_proj runs as ONE GEMM
+    (N = 3C); otherwise q rows [0,C) of in_proj act on q_in and rows [C,3C) on kv_in.
+    Attention-probability dropout p_attn uses the in-kernel counter mask.
+    """
+
+    @staticmethod
+    def forward(ctx, q_in, kv_in, in_w, in_b, out_w, out_b, residual, n_head: int,
+                self_attn: bool, p_attn: float, p_out: float, seed: int):
+        B, Tq, C = q_in.shape
+        Tk = kv_in.shape[1]
+        q2 = q_in.reshape(B * Tq, C).to(BF16).contiguous()
+        if self_attn:
+            qkv = K.linear(q2, in_w, in_b)
+            p3 = qkv.view(B, Tq, 3 * C)
+            qv, kv_, vv = p3[:, :, :C], p3[:, :, C:2 * C], p3[:, :, 2 * C:]
+            kv2 = None
+            qp = kvp = None
+        else:
+            kv2 = kv_in.reshape(B * Tk, C).to(BF16).contiguous()
+            qp = K.linear(q2, in_w[:C], in_b[:C])
+            kvp = K.linear(kv2, in_w[C:], in_b[C:])
+            q3 = qp.view(B, Tq, C)
+            k3 = kvp.view(B, Tk, 2 * C)
+            qv, kv_, vv = q3, k3[:, :, :C], k3[:, :, C:]
+            qkv = None
+        sa = seed ^ 0x5A5A5A5A
+        o, lse = K.attn_fwd(qv, kv_, vv, n_head, False, drop_p=p_attn, seed=sa)
+        r2 = residual.reshape(B * Tq, C).to(BF16).contiguous()
+        out = K.linear(o.view(B * Tq, C), out_w, out_b, residual=r2, drop_p=p_out, seed=seed)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse)
+            ctx.cfg = (B, Tq, Tk, C, n_head, self_attn, p_attn, p_out, seed, sa)
+        return out.view(B, Tq, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse = ctx.saved_tensors
+        B, Tq, Tk, C, H, self_attn, p_attn, p_out, seed, sa = ctx.cfg
+        d2 = dout.reshape(B * Tq, C).to(BF16).contiguous()
+        dres = dout if _need(ctx, 6) else None
+        dbr = K.dropout_mask_apply(d2, p_out, seed) if p_out > 0 else d2
+        d_out_w = K.linear_dw(dbr, o.view(B * Tq, C)) if _need(ctx, 4) else None
+        d_out_b = K.colsum(dbr) if _need(ctx, 5) else None
+        do = K.linear_dx(dbr, out_w).view(B, Tq, C)
+        din_w = torch.empty_like(in_w) if _need(ctx, 2) else None
+        din_b = torch.empty(3 * C, dtype=BF16, device=d2.device) if _need(ctx, 3) else None
+        dq_in = dkv_in = None
+        if self_attn:
+            p3 = qkv.view(B, Tq, 3 * C)
+            dqkv = torch.empty(B * Tq, 3 * C, dtype=BF16, device=d2.device)
+            dp3 = dqkv.view(B, Tq, 3 * C)
+            K.attn_bwd(do, p3[:, :, :C], p3[:, :, C:2 * C], p3[:, :, 2 * C:], o, lse, H, False,
+                       dp3[:, :, :C], dp3[:, :, C:2 * C], dp3[:, :, 2 * C:], drop_p=p_attn,
+                       seed=sa)
+            if din_w is not None:
+                K.linear_dw(dqkv, q2, out=din_w)
+            if din_b is not None:
+                K.colsum(dqkv, out=din_b)
+            if _need(ctx, 0):
+                dq_in = K.linear_dx(dqkv, in_w).view(B, Tq, C)
+        else:
+            q3 = qp.view(B, Tq, C)
+            k3 = kvp.view(B, Tk, 2 * C)
+            dqp = torch.empty(B * Tq, C, dtype=BF16, device=d2.device)
+            dkvp = torch.empty(B * Tk, 2 * C, dtype=BF16, device=d2.device)
+            dk3 = dkvp.view(B, Tk, 2 * C)
+            K.attn_bwd(do, q3, k3[:, :, :C], k3[:, :, C:], o, lse, H, False, dqp.view(B, Tq, C),
+                       dk3[:, :, :C], dk3[:, :, C:], drop_p=p_attn, seed=sa)
+            if din_w is not None:
+                K.linear_dw(dqp, q2, out=din_w[:C])
+                K.linear_dw(dkvp, kv2, out=din_w[C:])
+            if din_b is not None:
+                K.colsum(dqp, out=din_b[:C])
+                K.colsum(dkvp, out=din_b[C:])
+            if _need(ctx, 0):
+                dq_in = K.linear_dx(dqp, in_w[:C]).view(B, Tq, C)
+            if _need(ctx, 1):
+                dkv_in = K.linear_dx(dkvp, in_w[C:]).view(B, Tk, C)
+        return dq_in, dkv_in, din_w, din_b, d_out_w, d_out_b, dres, None, None, None, None, None
+
+
+class CrossAttnFn(torch.autograd.Function):
+    """Gated cross-attention residual of the cross-att bridge (gpt2_cross-att/model.py:46-58,
+    :99-101): x + tanh(g) * c_proj(SDPA(q_proj(ln_x x), kv_proj(z)))."""
+
+    @staticmethod
+    def forward(ctx, x, z, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b, gate, n_head: int):
+        B, T, C = x.shape
+        S = z.shape[1]
+        x2 = x.reshape(B * T, C).contiguous()
+        z2 = z.reshape(B * S, C).to(BF16).contiguous()
+        xn, mean, rstd = K.layernorm_fwd(x2, ln_w, ln_b)
+        qp = K.linear(xn, q_w, q_b)
+        kvp = K.linear(z2, kv_w, kv_b)
+        k3 = kvp.view(B, S, 2 * C)
+        o, lse = K.attn_fwd(qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], n_head, False)
+        ybr = torch.empty(B * T, C, dtype=BF16, device=x.device)
+        out = K.linear(o.view(B * T, C), c_w, c_b, residual=x2, gate=gate, pre_out=ybr)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w,
+                                  c_w, gate)
+            ctx.cfg = (B, T, S, C, n_head)
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w, c_w,
+         gate) = ctx.saved_tensors
+        B, T, S, C, H = ctx.cfg
+        d2 = dout.reshape(B * T, C).to(BF16).contiguous()
+        g = [None] * 12
+        gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
+        dbr = K.gate_bwd(d2, ybr, gate, gacc)
+        if _need(ctx, 10):
+            g[10] = gacc.to(gate.dtype).view_as(gate)
+        if _need(ctx, 8):
+            g[8] = K.linear_dw(dbr, o.view(B * T, C))
+        if _need(ctx, 9):
+            g[9] = K.colsum(dbr)
+        do = K.linear_dx(dbr, c_w).view(B, T, C)
+        dqp = torch.empty(B * T, C, dtype=BF16, device=d2.device)
+        dkvp = torch.empty(B * S, 2 * C, dtype=BF16, device=d2.device)
+        k3 = kvp.view(B, S, 2 * C)
+        dk3 = dkvp.view(B, S, 2 * C)
+        K.attn_bwd(do, qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], o, lse, H, False,
+                   dqp.view(B, T, C), dk3[:, :, :C], dk3[:, :, C:])
+        if _need(ctx, 4):
+            g[4] = K.linear_dw(dqp, xn)
+        if _need(ctx, 5):
+            g[5] = K.colsum(dqp)
+        if _need(ctx, 6):
+            g[6] = K.linear_dw(dkvp, z2)
+        if _need(ctx, 7):
+            g[7] = K.colsum(dkvp)
+        if _need(ctx, 1):
+            g[1] = K.linear_dx(dkvp, kv_w).view(B, S, C)
+        dxn = K.linear_dx(dqp, q_w)
+        dx = d2.clone()
+        dw = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 2) else None
+        db = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 3) else None
+        K.layernorm_bwd(dxn, x2, ln_w, mean, rstd, dx=dx, accumulate_dx=True, dw=dw, db=db)
+        g[2], g[3] = dw, db
+        g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
+        return tuple(g)
+
+
+# ------------------------------------------------------------------------ embeddings
+class EmbedFn(torch.autograd.Function):
+    """wte(idx) + wpe(arange(T)) written at row offset `off` of a [B, S, C] buffer whose
+    first `off` rows per sequence are `prefix` (the caption image tokens; may be None)."""
+
+    @staticmethod
+    def forward(ctx, idx, wte, wpe, prefix=None):
+        B, T = idx.shape
+        C = wte.shape[1]
+        M = 0 if prefix is None else prefix.shape[1]
+        S = M + T
+        out = torch.empty(B, S, C, dtype=BF16, device=idx.device)
+        if prefix is not None:
+            out[:, :M].copy_(prefix)
+        K.embedding_fwd(idx, wte, wpe, out, T, S, M)
+        if torch.is_grad_enabled():
+            ctx.save_for_backward(idx)
+            ctx.cfg = (B, T, C, M, S, wte.shape[0], wpe.shape[0], wte.dtype, wpe.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        B, T, C, M, S, V, P, dt_te, dt_pe = ctx.cfg
+        dout = dout.to(BF16).contiguous()
+        dwte = dwpe = dprefix = None
+        if _need(ctx, 1) or _need(ctx, 2):
+            acc_te = torch.zeros(V, C, dtype=torch.float32, device=dout.device) if _need(ctx, 1) else None
+            acc_pe = torch.zeros(P, C, dtype=torch.float32, device=dout.device) if _need(ctx, 2) else None
+            K.embedding_bwd(idx, dout, acc_te, acc_pe, T, S, M, C)
+            if acc_te is not None:
+                dwte = acc_te.to(dt_te)
+            if acc_pe is not None:
+                dwpe = acc_pe.to(dt_pe)
+        if M > 0 and _need(ctx, 3):
+            dprefix = dout[:, :M]
+        return None, dwte, dwpe, dprefix
+
+
+# -------------------------------------------------------------- lm_head + cross-entropy
+class LMHeadLossFn(torch.autograd.Function):
+    """logits = x W^T (tied wte), loss = CE(logits[:, off:off+T], targets) in one unit.
+
+    The CE kernel reads the loss rows of the logits in place and emits
+    dlogits = softmax - onehot at forward time; backward is two GEMMs scaled on the
+    device by grad_loss / count (no host sync).  Logits are returned non-differentiable.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, targets, row_offset: int, mask=None, mask_mode: bool = False):
+        B, S, C = x.shape
+        T = targets.shape[1]
+        x2 = x.reshape(B * S, C).to(BF16).contiguous()
+        logits = K.linear(x2, w)
+        V = w.shape[0]
+        need = torch.is_grad_enabled() and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        out, dl = K.cross_entropy(logits, targets, rows_per_group=T, group_stride=S,
+                                  row_offset=row_offset, mask=mask, mask_mode=mask_mode,
+                                  want_grad=need)
+        loss = out[0].clone()
+        logits = logits.view(B, S, V)
+        ctx.mark_non_differentiable(logits)
+        if need:
+            ctx.save_for_backward(x2, w, dl, out)
+            ctx.cfg = (B, S, T, C, row_offset)
+        return logits, loss
+
+    @staticmethod
+    def backward(ctx, _dlogits, dloss):
+        x2, w, dl, out = ctx.saved_tensors
+        B, S, T, C, off = ctx.cfg
+        scale = (dloss.float().reshape(1) * out[1:2]).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dxt = K.gemm(dl, w, b_mn=True, alpha_ptr=scale)
+            if off == 0 and T == S:
+                dx = dxt.view(B, S, C)
+            else:
+                dx = torch.zeros(B, S, C, dtype=BF16, device=dl.device)
+                dx[:, off:off + T] = dxt.view(B, T, C)
+        if ctx.needs_input_grad[1]:
+            if off == 0 and T == S:
+                xt = x2
+            else:
+                xt = x2.view(B, S, C)[:, off:off + T].reshape(B * T, C).contiguous()
+            dw = K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale)
+        return dx, dw, None, None, None, None
+
+
+def pool_clip(tokens):
+    """pool_clip_197_to_33_avg_with_cls on the GPU (gpt2_linear/model.py:240-254)."""
+    return K.pool_clip(tokens)

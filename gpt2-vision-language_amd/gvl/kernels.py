@@ -1,0 +1,310 @@
+"""Typed Python wrappers over the libgvl C-ABI (one function per entry point of include/gvl.h).
+
+Every wrapper takes torch tensors that already live on the current ROCm device, checks
+dtype/layout on the host, and launches on torch.cuda.current_stream().  There is no CPU
+path: a CPU tensor is rejected with a clear error.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib
+from ._lib import AttnBwdDesc, AttnDesc, GemmDesc
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _L():
+    return _lib.lib()
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "gvl: the HIP kernel path needs tensors on a ROCm GPU (got a CPU tensor); "
+                "there is no CPU fallback in the product path")
+
+
+def _rowmajor(t, name):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"gvl: {name} must be a 2-D row-major view (got shape {tuple(t.shape)}, "
+                         f"strides {t.stride()})")
+
+
+# ------------------------------------------------------------------------------- GEMM
+def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, bias=None,
+         act=0, dact=0, pre_out=None, pre_in=None, residual=None, gate=None, drop_p=0.0,
+         seed=0, out_dtype=BF16):
+    """C = epi(alpha * opA @ opB).  a: [M,K] (a_mn=False) or [K,M]; b: [N,K] (b_mn=False,
+    nn.Linear weight) or [K,N].  Returns C [M,N]."""
+    _dev(a, b)
+    _rowmajor(a, "A")
+    _rowmajor(b, "B")
+    if a.dtype != BF16 or b.dtype != BF16:
+        raise TypeError("gvl.gemm: operands must be bf16")
+    M, K = (a.shape[1], a.shape[0]) if a_mn else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if b_mn else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gvl.gemm: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    _rowmajor(out, "C")
+    d = GemmDesc()
+    d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    d.m, d.n, d.k = M, N, K
+    d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), out.stride(0)
+    d.a_mn, d.b_mn = int(a_mn), int(b_mn)
+    d.alpha = float(alpha)
+    d.alpha_ptr = _p(alpha_ptr)
+    d.bias = _p(bias)
+    d.act, d.dact = int(act), int(dact)
+    d.pre_out = _p(pre_out)
+    d.pre_in = _p(pre_in)
+    pre = pre_out if pre_out is not None else pre_in
+    d.ldp = pre.stride(0) if pre is not None else 0
+    d.residual = _p(residual)
+    d.ldr = residual.stride(0) if residual is not None else 0
+    d.gate = _p(gate)
+    d.drop_p = float(drop_p)
+    d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    d.c_fp32 = int(out.dtype == F32)
+    _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
+    return out
+
+
+def linear(x2, w, bias=None, **kw):
+    """y = x2 @ w.T (+bias) — nn.Linear forward on a [rows, in] view."""
+    return gemm(x2, w, bias=bias, **kw)
+
+
+def linear_dx(dy2, w, **kw):
+    """dx = dy2 @ w — nn.Linear input gradient (w stored [out, in] is MN-major here)."""
+    return gemm(dy2, w, b_mn=True, **kw)
+
+
+def linear_dw(dy2, x2, **kw):
+    """dW = dy2.T @ x2 — nn.Linear weight gradient ([out, in])."""
+    return gemm(dy2, x2, a_mn=True, b_mn=True, **kw)
+
+
+# ------------------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x2, w, b, eps=1e-5, out=None, stats=True):
+    _dev(x2)
+    _rowmajor(x2, "x")
+    rows, cols = x2.shape
+    if out is None:
+        out = torch.empty(rows, cols, dtype=BF16, device=x2.device)
+    mean = torch.empty(rows, dtype=F32, device=x2.device) if stats else None
+    rstd = torch.empty(rows, dtype=F32, device=x2.device) if stats else None
+    _lib.check(_L().gvl_layernorm_fwd(x2.data_ptr(), x2.stride(0), w.data_ptr(), b.data_ptr(),
+                                      out.data_ptr(), out.stride(0), _p(mean), _p(rstd), rows, cols,
+                                      float(eps), _stream()), "gvl_layernorm_fwd")
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy2, x2, w, mean, rstd, dx=None, accumulate_dx=False, dw=None, db=None,
+                  accumulate_wb=False):
+    rows, cols = x2.shape
+    if dx is None:
+        dx = torch.empty(rows, cols, dtype=BF16, device=x2.device)
+    ws = None
+    if dw is not None or db is not None:
+        n = _L().gvl_layernorm_bwd_workspace_size(rows, cols)
+        ws = torch.empty(max(n, 4) // 4, dtype=F32, device=x2.device)
+    _lib.check(_L().gvl_layernorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
+                                      w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                      dx.stride(0), int(accumulate_dx), _p(dw), _p(db),
+                                      int(accumulate_wb), _p(ws), rows, cols, _stream()),
+               "gvl_layernorm_bwd")
+    return dx
+
+
+# ------------------------------------------------------------------------- attention
+def _bthd(t, T, H):
+    """strides (b, t, h) of a [B, T, *] tensor whose head h occupies cols h*64..h*64+63."""
+    return t.stride(0), t.stride(1), 64
+
+
+def attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p=0.0, seed=0):
+    d = AttnDesc()
+    d.q, d.k, d.v, d.o, d.lse = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), _p(lse)
+    d.B, d.H, d.Tq, d.Tk = B, H, Tq, Tk
+    d.q_sb, d.q_st, d.q_sh = q.stride(0), q.stride(1), 64
+    d.k_sb, d.k_st, d.k_sh = k.stride(0), k.stride(1), 64
+    d.v_sb, d.v_st, d.v_sh = v.stride(0), v.stride(1), 64
+    d.o_sb, d.o_st, d.o_sh = o.stride(0), o.stride(1), 64
+    d.causal = int(causal)
+    d.scale = float(scale)
+    d.drop_p = float(drop_p)
+    d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return d
+
+
+def attn_fwd(q, k, v, H, causal, scale=None, drop_p=0.0, seed=0, out=None):
+    """q: [B,Tq,*] view whose cols h*64.. are head h (e.g. a slice of packed qkv);
+    k, v: [B,Tk,*].  Returns (o [B,Tq,H*64] bf16, lse [B,H,Tq] fp32)."""
+    _dev(q, k, v)
+    for t in (q, k, v):
+        if t.dtype != BF16 or t.stride(2) != 1:
+            raise ValueError("gvl.attn_fwd: q/k/v must be bf16 with unit last stride")
+    B, Tq = q.shape[0], q.shape[1]
+    Tk = k.shape[1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(64)
+    if out is None:
+        out = torch.empty(B, Tq, H * 64, dtype=BF16, device=q.device)
+    lse = torch.empty(B, H, Tq, dtype=F32, device=q.device)
+    d = attn_desc(q, k, v, out, lse, B, H, Tq, Tk, causal, scale, drop_p, seed)
+    _lib.check(_L().gvl_attn_fwd(C.byref(d), _stream()), "gvl_attn_fwd")
+    return out, lse
+
+
+def attn_bwd(dout, q, k, v, o, lse, H, causal, dq, dk, dv, scale=None, drop_p=0.0, seed=0):
+    """Writes dq/dk/dv (views with the layouts of q/k/v)."""
+    B, Tq = q.shape[0], q.shape[1]
+    Tk = k.shape[1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(64)
+    d = attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p, seed)
+    g = AttnBwdDesc()
+    g.dout, g.do_sb, g.do_st, g.do_sh = dout.data_ptr(), dout.stride(0), dout.stride(1), 64
+    g.dq, g.dq_sb, g.dq_st, g.dq_sh = dq.data_ptr(), dq.stride(0), dq.stride(1), 64
+    g.dk, g.dk_sb, g.dk_st, g.dk_sh = dk.data_ptr(), dk.stride(0), dk.stride(1), 64
+    g.dv, g.dv_sb, g.dv_st, g.dv_sh = dv.data_ptr(), dv.stride(0), dv.stride(1), 64
+    n = _L().gvl_attn_bwd_workspace_size(C.byref(d))
+    ws = torch.empty(max(n, 4) // 4, dtype=F32, device=q.device)
+    g.workspace = ws.data_ptr()
+    _lib.check(_L().gvl_attn_bwd(C.byref(d), C.byref(g), _stream()), "gvl_attn_bwd")
+
+
+# ---------------------------------------------------------------------- cross entropy
+def cross_entropy(logits2, targets, *, rows_per_group=None, group_stride=0, row_offset=0,
+                  mask=None, mask_mode=False, want_grad=True):
+    """Returns (loss_and_inv [2] fp32 device tensor, dlogits [rows, V] bf16 or None)."""
+    _dev(logits2, targets)
+    V = logits2.shape[1]
+    rows = targets.numel()
+    if rows_per_group is None:
+        rows_per_group = max(rows, 1)
+    tg = targets.reshape(-1)
+    if tg.dtype != torch.int64:
+        tg = tg.long()
+    tg = tg.contiguous()
+    mk = None
+    if mask is not None:
+        mk = mask.reshape(-1).to(torch.uint8).contiguous()
+    row_loss = torch.empty(max(rows, 1), dtype=F32, device=logits2.device)
+    dl = torch.empty(rows, V, dtype=BF16, device=logits2.device) if want_grad else None
+    out = torch.empty(2, dtype=F32, device=logits2.device)
+    _lib.check(_L().gvl_cross_entropy(logits2.data_ptr(), logits2.stride(0), rows, V,
+                                      rows_per_group, group_stride, row_offset, tg.data_ptr(),
+                                      _p(mk), int(mask_mode), row_loss.data_ptr(), _p(dl),
+                                      dl.stride(0) if dl is not None else 0, out.data_ptr(),
+                                      _stream()), "gvl_cross_entropy")
+    return out, dl
+
+
+# -------------------------------------------------------------------------- embedding
+def embedding_fwd(idx, wte, wpe, out, T, out_rows_per_seq, out_offset):
+    _dev(idx, wte, wpe, out)
+    idx = idx.contiguous()
+    C_ = wte.shape[1]
+    _lib.check(_L().gvl_embedding_fwd(idx.data_ptr(), wte.data_ptr(), wpe.data_ptr(),
+                                      out.data_ptr(), idx.numel(), T, C_, out_rows_per_seq,
+                                      out_offset, _stream()), "gvl_embedding_fwd")
+    return out
+
+
+def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset, C_):
+    idx = idx.contiguous()
+    _lib.check(_L().gvl_embedding_bwd(idx.data_ptr(), dout.data_ptr(), _p(dwte_acc),
+                                      _p(dwpe_acc), idx.numel(), T, C_, out_rows_per_seq,
+                                      out_offset, _stream()), "gvl_embedding_bwd")
+
+
+# ------------------------------------------------------------------------------- pool
+def pool_clip(tokens, out_dtype=None):
+    """[B, 1+s*s, D] -> [B, 33, D]: CLS + adaptive-avg (4,8) + L2 normalise."""
+    _dev(tokens)
+    t = tokens.contiguous()
+    if t.dtype not in (F32, BF16):
+        t = t.float()
+    B, L, D = t.shape
+    out_dtype = out_dtype or t.dtype
+    out = torch.empty(B, 33, D, dtype=out_dtype, device=t.device)
+    _lib.check(_L().gvl_pool_clip(t.data_ptr(), int(t.dtype == F32), out.data_ptr(),
+                                  int(out_dtype == F32), B, L, D, _stream()), "gvl_pool_clip")
+    return out
+
+
+# ------------------------------------------------------------------------- optimizer
+def grad_norm(g_flat, max_norm, out=None):
+    _dev(g_flat)
+    n = g_flat.numel()
+    ws = torch.empty(max(_L().gvl_grad_norm_workspace_size(n), 4) // 4, dtype=F32,
+                     device=g_flat.device)
+    if out is None:
+        out = torch.empty(2, dtype=F32, device=g_flat.device)
+    _lib.check(_L().gvl_grad_norm(g_flat.data_ptr(), n, float(max_norm), ws.data_ptr(),
+                                  out.data_ptr(), _stream()), "gvl_grad_norm")
+    return out
+
+
+def adamw(p, g, m, v, n_decay, lr, beta1, beta2, eps, wd, step, grad_scale=None):
+    _dev(p, g, m, v)
+    _lib.check(_L().gvl_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                              int(n_decay), float(lr), float(beta1), float(beta2), float(eps),
+                              float(wd), int(step), _p(grad_scale), _stream()), "gvl_adamw")
+
+
+# ------------------------------------------------------------------------- elementwise
+def colsum(x2, out=None, accumulate=False):
+    rows, cols = x2.shape
+    if out is None:
+        out = torch.empty(cols, dtype=BF16, device=x2.device)
+    ws = torch.empty(max(_L().gvl_colsum_workspace_size(rows, cols), 4) // 4, dtype=F32,
+                     device=x2.device)
+    _lib.check(_L().gvl_colsum(x2.data_ptr(), rows, cols, x2.stride(0), out.data_ptr(),
+                               int(accumulate), ws.data_ptr(), _stream()), "gvl_colsum")
+    return out
+
+
+def dropout_mask_apply(x2, p, seed, out=None):
+    rows, cols = x2.shape
+    if out is None:
+        out = torch.empty(rows, cols, dtype=BF16, device=x2.device)
+    _lib.check(_L().gvl_dropout_mask_apply(x2.data_ptr(), x2.stride(0), out.data_ptr(),
+                                           out.stride(0), rows, cols, float(p),
+                                           int(seed) & 0xFFFFFFFFFFFFFFFF, _stream()),
+               "gvl_dropout_mask_apply")
+    return out
+
+
+def gate_bwd(dx, y, gate, gate_grad_f32):
+    n = dx.numel()
+    dy = torch.empty_like(dx)
+    ws = torch.empty(max(_L().gvl_gate_bwd_workspace_size(n), 4) // 4, dtype=F32,
+                     device=dx.device)
+    _lib.check(_L().gvl_gate_bwd(dx.data_ptr(), y.data_ptr(), gate.data_ptr(), dy.data_ptr(),
+                                 gate_grad_f32.data_ptr(), n, ws.data_ptr(), _stream()),
+               "gvl_gate_bwd")
+    return dy
+
+
+def f32_to_bf16(x, out, accumulate=False):
+    _lib.check(_L().gvl_f32_to_bf16(x.data_ptr(), out.data_ptr(), x.numel(), int(accumulate),
+                                    _stream()), "gvl_f32_to_bf16")
+    return out

@@ -1,0 +1,175 @@
+"""Fused AdamW + gradient clipping over flat bf16 arenas (the reference's
+torch.optim.AdamW(fused=True) + clip_grad_norm_, train_gpt2.py:140-143, :472, :476).
+
+MI355X design: at the first step every trainable parameter (and its .grad) is re-pointed
+into ONE contiguous bf16 arena per quantity (params, grads, exp_avg, exp_avg_sq), laid out
+group by group (decay group first).  Then
+  * the global grad norm is one streaming reduction over the grad arena, finished on the
+    device together with the clip coefficient (no host sync);
+  * AdamW is one streaming kernel per param group, applying the clip coefficient to the
+    gradient on the fly (14 B of HBM traffic per parameter);
+  * data-parallel gradient buckets are plain slices of the grad arena (gvl.dist).
+Parameters keep their identity; `param.data` / `param.grad` become views of the arenas.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+_ALIGN = 8  # elements: every segment starts 16-byte aligned
+
+
+def _pad(n):
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class AdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self._arena = None
+        self._clip_coef = None
+        self._step_count = 0
+
+    # ---------------------------------------------------------------- arenas
+    def _build(self):
+        params = [p for g in self.param_groups for p in g["params"]]
+        if not params:
+            raise ValueError("gvl AdamW: no parameters")
+        dev = params[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("gvl AdamW runs on the ROCm device; use torch.optim.AdamW on CPU")
+        for p in params:
+            if p.dtype != BF16:
+                raise TypeError("gvl AdamW expects bf16 parameters (the reference trains the "
+                                "model after .to(torch.bfloat16))")
+        offs, seg = [], []
+        total = 0
+        for g in self.param_groups:
+            start = total
+            for p in g["params"]:
+                offs.append(total)
+                total += _pad(p.numel())
+            seg.append((start, total))
+        total = max(total, _ALIGN)
+        parena = torch.zeros(total, dtype=BF16, device=dev)
+        garena = torch.zeros(total, dtype=BF16, device=dev)
+        marena = torch.zeros(total, dtype=BF16, device=dev)
+        varena = torch.zeros(total, dtype=BF16, device=dev)
+        for p, o in zip(params, offs):
+            n = p.numel()
+            view = parena[o:o + n].view_as(p)
+            view.copy_(p.data)
+            p.data = view
+            gview = garena[o:o + n].view_as(p)
+            if p.grad is not None:
+                gview.copy_(p.grad)
+            p.grad = gview
+            st = self.state[p]
+            st["step"] = torch.zeros((), dtype=torch.float32)
+            st["exp_avg"] = marena[o:o + n].view_as(p)
+            st["exp_avg_sq"] = varena[o:o + n].view_as(p)
+        self._arena = dict(p=parena, g=garena, m=marena, v=varena, offs=offs, seg=seg,
+                           params=params)
+
+    @property
+    def grad_arena(self):
+        if self._arena is None:
+            self._build()
+        return self._arena["g"]
+
+    def arena_layout(self):
+        """[(param, offset, numel)] in arena order (used by gvl.dist buckets)."""
+        if self._arena is None:
+            self._build()
+        a = self._arena
+        return [(p, o, p.numel()) for p, o in zip(a["params"], a["offs"])]
+
+    def _sync_grads(self):
+        """Re-point any grad that autograd replaced (e.g. after set_to_none)."""
+        a = self._arena
+        for p, o in zip(a["params"], a["offs"]):
+            n = p.numel()
+            gview = a["g"][o:o + n].view_as(p)
+            if p.grad is None:
+                gview.zero_()
+                p.grad = gview
+            elif p.grad.data_ptr() != gview.data_ptr():
+                gview.copy_(p.grad)
+                p.grad = gview
+
+    # -------------------------------------------------------------- API
+    def zero_grad(self, set_to_none: bool = True):
+        """Zero the grad arena in one memset; grads stay arena views (set_to_none ignored)."""
+        if self._arena is None:
+            self._build()
+        self._arena["g"].zero_()
+        self._sync_grads()
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float):
+        """Global L2 norm of all grads + the clip coefficient, both on the device; the
+        coefficient is applied by the next step() (fused).  Returns the norm (0-dim fp32)."""
+        if self._arena is None:
+            self._build()
+        self._sync_grads()
+        out = K.grad_norm(self._arena["g"], max_norm)
+        self._clip_coef = out[1:2]
+        return out[0]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        if self._arena is None:
+            self._build()
+        self._sync_grads()
+        self._step_count += 1
+        a = self._arena
+        for g, (s0, s1) in zip(self.param_groups, a["seg"]):
+            if s1 == s0:
+                continue
+            b1, b2 = g["betas"]
+            K.adamw(a["p"][s0:s1], a["g"][s0:s1], a["m"][s0:s1], a["v"][s0:s1], s1 - s0,
+                    g["lr"], b1, b2, g["eps"], g["weight_decay"], self._step_count,
+                    grad_scale=self._clip_coef)
+        for p in a["params"]:
+            self.state[p]["step"].fill_(self._step_count)
+        self._clip_coef = None
+        return loss
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self._arena is not None:
+            a = self._arena
+            for p, o in zip(a["params"], a["offs"]):
+                n = p.numel()
+                st = self.state[p]
+                for key, arena in (("exp_avg", a["m"]), ("exp_avg_sq", a["v"])):
+                    view = arena[o:o + n].view_as(p)
+                    if st[key].data_ptr() != view.data_ptr():
+                        view.copy_(st[key])
+                        st[key] = view
+                self._step_count = int(st["step"].item())
+
+
+def clip_grad_norm_(optimizer_or_params, max_norm: float):
+    """Drop-in for torch.nn.utils.clip_grad_norm_.  Given a gvl AdamW, computes the norm on
+    the device and defers the scaling into the fused step; otherwise falls back to torch's
+    utility on the given parameters (eager, not the hot path)."""
+    if isinstance(optimizer_or_params, AdamW):
+        return optimizer_or_params.clip_grad_norm_(max_norm)
+    return torch.nn.utils.clip_grad_norm_(optimizer_or_params, max_norm)
+
+
+def get_lr(it, max_lr, min_lr, warmup_steps, max_steps):
+    """Cosine schedule with linear warmup (train_gpt2.py:277-285)."""
+    import math
+    if it < warmup_steps:
+        return max_lr * (it + 1) / warmup_steps
+    if it > max_steps:
+        return min_lr
+    ratio = (it - warmup_steps) / (max_steps - warmup_steps)
+    assert 0 <= ratio <= 1
+    return min_lr + 0.5 * (1.0 + math.cos(math.pi * ratio)) * (max_lr - min_lr)

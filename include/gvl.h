@@ -39,6 +39,7 @@ int gvl_abi_version(void);
  *   opA: a_mn=0 -> A stored [M][K] (row stride lda);  a_mn=1 -> A stored [K][M].
  *   opB: b_mn=0 -> B stored [N][K] (nn.Linear weight); b_mn=1 -> B stored [K][N].
  * Epilogue order: *alpha_ptr, +bias[n], *dgelu(pre_in), {pre_out=v; v=gelu(v)},
+ *   (with gate and no act, pre_out receives the un-gated branch),
  *   dropout(p, seed, index m*N+n), *tanh(*gate), +residual, store (bf16 or fp32).
  * Replaces: nn.Linear forward/backward (addmm/mm) at source/gpt2/train_gpt2.py:26-27,
  *   50-58,96-97; gpt2_linear/model.py:125-129,172; gpt2_cross-att/model.py:39-41,81;

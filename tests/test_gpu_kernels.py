@@ -1,0 +1,344 @@
+"""Per-kernel parity on the MI355X: every libgvl entry point vs the CPU oracle.
+
+Inputs are rounded to bf16 first and the oracle runs in fp32 on the rounded values, so the
+tolerances measure only the kernels' own rounding (bf16 outputs: ~2^-8 relative).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as O
+from tests.helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _k():
+    from gvl import kernels as K
+    return K
+
+
+def _r(t):
+    """round to bf16, back to fp32 CPU"""
+    return t.to(BF).float().cpu()
+
+
+def keep_mask(seed, idx, p):
+    """numpy restatement of common.h rng_keep (splitmix64 finaliser)."""
+    G, M1, M2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (idx.astype(np.uint64) + np.uint64(1)) * G
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        z = z ^ (z >> np.uint64(31))
+    u = z >> np.uint64(32)
+    thresh = np.uint64(int(float(np.float32(p)) * 4294967296.0))
+    return u >= thresh
+
+
+# ------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 192), (200, 136, 72), (8, 8, 8), (130, 264, 1000)])
+def test_gemm_layouts(cuda, a_mn, b_mn, M, N, K):
+    if (a_mn and M % 8) or (b_mn and N % 8):
+        pytest.skip("MN-major operands need multiples of 8")
+    K_ = _k()
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K).to(BF)
+    b = torch.randn(K, N).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    c = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn))
+    ref = a.float() @ b.float()
+    assert rel_err(c.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_gemm_epilogue_act_bias_residual(cuda, act):
+    K_ = _k()
+    torch.manual_seed(act)
+    M, N, Kd = 192, 256, 384
+    x = torch.randn(M, Kd).to(BF)
+    w = (torch.randn(N, Kd) * 0.05).to(BF)
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    pre = torch.empty(M, N, dtype=BF, device=cuda)
+    y = K_.gemm(x.to(cuda), w.to(cuda), bias=bias.to(cuda), act=act, pre_out=pre,
+                residual=res.to(cuda))
+    h = x.float() @ w.float().t() + bias.float()
+    g = O.gelu_tanh(h) if act == 1 else O.gelu_erf(h)
+    assert rel_err(pre.float().cpu().numpy(), h.numpy()) < 8e-3
+    assert rel_err(y.float().cpu().numpy(), (g + res.float()).numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("dact", [1, 2])
+def test_gemm_dgelu_alpha_ptr(cuda, dact):
+    K_ = _k()
+    torch.manual_seed(10 + dact)
+    M, N, Kd = 128, 192, 256
+    dy = torch.randn(M, Kd).to(BF)
+    w = (torch.randn(Kd, N) * 0.05).to(BF)  # nn.Linear weight [out=Kd][in=N]
+    hpre = torch.randn(M, N).to(BF)
+    alpha = torch.tensor([0.37], dtype=torch.float32)
+    out = K_.gemm(dy.to(cuda), w.to(cuda), b_mn=True, dact=dact, pre_in=hpre.to(cuda),
+                  alpha_ptr=alpha.to(cuda))
+    hx = hpre.float().requires_grad_(True)
+    (O.gelu_tanh(hx) if dact == 1 else O.gelu_erf(hx)).sum().backward()
+    ref = 0.37 * (dy.float() @ w.float()) * hx.grad
+    assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
+def test_gemm_dropout_gate(cuda):
+    K_ = _k()
+    torch.manual_seed(3)
+    M, N, Kd = 96, 128, 64
+    x = torch.randn(M, Kd).to(BF)
+    w = (torch.randn(N, Kd) * 0.1).to(BF)
+    res = torch.randn(M, N).to(BF)
+    gate = torch.tensor(0.7).to(BF)
+    ybr = torch.empty(M, N, dtype=BF, device=cuda)
+    p, seed = 0.1, 987654321
+    y = K_.gemm(x.to(cuda), w.to(cuda), residual=res.to(cuda), gate=gate.to(cuda),
+                pre_out=ybr, drop_p=p, seed=seed)
+    h = x.float() @ w.float().t()
+    keep = torch.from_numpy(keep_mask(seed, np.arange(M * N), p).reshape(M, N))
+    hd = torch.where(keep, h / (1 - p), torch.zeros_like(h))
+    ref = res.float() + math.tanh(float(gate.float())) * hd
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+    assert rel_err(ybr.float().cpu().numpy(), hd.numpy()) < 8e-3
+    frac = 1 - keep.float().mean().item()
+    assert 0.08 < frac < 0.12
+
+
+# ------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("rows,C", [(37, 128), (300, 768), (5, 1024)])
+def test_layernorm_fwd_bwd(cuda, rows, C):
+    K_ = _k()
+    torch.manual_seed(rows)
+    x = (torch.randn(rows, C) * 2 + 0.5).to(BF)
+    w = (1 + 0.1 * torch.randn(C)).to(BF)
+    b = (0.1 * torch.randn(C)).to(BF)
+    y, mean, rstd = K_.layernorm_fwd(x.to(cuda), w.to(cuda), b.to(cuda))
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = b.float().requires_grad_(True)
+    ref = O.layernorm(xr, wr, br)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    dy = torch.randn(rows, C).to(BF)
+    ref.backward(dy.float())
+    prev = torch.randn(rows, C).to(BF)
+    dx = prev.clone().to(cuda)
+    dw = torch.empty(C, dtype=BF, device=cuda)
+    db = torch.empty(C, dtype=BF, device=cuda)
+    K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd, dx=dx, accumulate_dx=True,
+                     dw=dw, db=db)
+    assert rel_err(dx.float().cpu().numpy(), (xr.grad + prev.float()).numpy()) < 1e-2
+    assert rel_err(dw.float().cpu().numpy(), wr.grad.numpy()) < 1e-2
+    assert rel_err(db.float().cpu().numpy(), br.grad.numpy()) < 1e-2
+
+
+# ------------------------------------------------------------------------- attention
+def _attn_case(cuda, B, H, Tq, Tk, causal, packed, drop_p=0.0, seed=0, grad=True):
+    K_ = _k()
+    torch.manual_seed(B * 100 + Tq + Tk)
+    C = H * 64
+    q = torch.randn(B, Tq, C).to(BF)
+    k = torch.randn(B, Tk, C).to(BF)
+    v = torch.randn(B, Tk, C).to(BF)
+    if packed:  # q, k, v as column slices of one [B, T, 3C] buffer (c_attn output)
+        buf = torch.cat([q, k, v], dim=2).to(cuda)
+        qg, kg, vg = buf[:, :, :C], buf[:, :, C:2 * C], buf[:, :, 2 * C:]
+    else:
+        qg, kg, vg = q.to(cuda), k.to(cuda), v.to(cuda)
+    o, lse = K_.attn_fwd(qg, kg, vg, H, causal, drop_p=drop_p, seed=seed)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    sq, sk, sv = (O.split_heads(t, H) for t in (qr, kr, vr))
+    if drop_p > 0:
+        s = (sq @ sk.transpose(-1, -2)) / 8.0
+        if causal:
+            s = s.masked_fill(~torch.ones(Tq, Tk, dtype=torch.bool).tril(), float("-inf"))
+        pr = torch.softmax(s, dim=-1)
+        idx = np.arange(B * H * Tq * Tk)
+        keep = torch.from_numpy(keep_mask(seed, idx, drop_p).reshape(B, H, Tq, Tk))
+        pr = torch.where(keep, pr / (1 - drop_p), torch.zeros_like(pr))
+        ref = O.merge_heads(pr @ sv)
+    else:
+        ref = O.merge_heads(O.attention(sq, sk, sv, causal))
+    assert rel_err(o.float().cpu().numpy(), ref.detach().numpy()) < 1.2e-2
+    if not grad:
+        return
+    do = torch.randn(B, Tq, C).to(BF)
+    ref.backward(do.float())
+    if packed:
+        dbuf = torch.empty(B, Tq, 3 * C, dtype=BF, device=cuda)
+        dq, dk, dv = dbuf[:, :, :C], dbuf[:, :, C:2 * C], dbuf[:, :, 2 * C:]
+    else:
+        dq = torch.empty(B, Tq, C, dtype=BF, device=cuda)
+        dk = torch.empty(B, Tk, C, dtype=BF, device=cuda)
+        dv = torch.empty(B, Tk, C, dtype=BF, device=cuda)
+    K_.attn_bwd(do.to(cuda), qg, kg, vg, o, lse, H, causal, dq, dk, dv, drop_p=drop_p, seed=seed)
+    for got, want, nm in ((dq, qr.grad, "dq"), (dk, kr.grad, "dk"), (dv, vr.grad, "dv")):
+        e = rel_err(got.float().cpu().numpy(), want.numpy())
+        assert e < 2.5e-2, f"{nm} rel err {e}"
+
+
+@pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (3, 12, 63), (2, 3, 64), (1, 1, 7)])
+def test_attention_causal(cuda, B, H, T):
+    _attn_case(cuda, B, H, T, T, True, packed=True)
+
+
+@pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257)])
+def test_attention_noncausal(cuda, Tq, Tk):
+    _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False)
+
+
+def test_attention_dropout_exact_mask(cuda):
+    _attn_case(cuda, 2, 2, 32, 33, False, packed=False, drop_p=0.1, seed=4242)
+
+
+def test_attention_matches_reference_fixture(cuda, golden):
+    """SDPA fixtures produced by the reference's torch path (tools/make_fixtures.py)."""
+    K_ = _k()
+    fx = golden("ops")
+    for name, causal in (("sdpa_causal", True), ("sdpa_cross", False), ("sdpa_self32", False)):
+        q, k, v = (torch.from_numpy(fx[f"{name}:{n}"]) for n in "qkv")
+        B, H = q.shape[0], q.shape[1]
+        to_bt = lambda t: t.transpose(1, 2).reshape(t.shape[0], t.shape[2], -1).to(BF).to(cuda)
+        o, _ = K_.attn_fwd(to_bt(q), to_bt(k), to_bt(v), H, causal)
+        want = torch.from_numpy(fx[f"{name}:o"]).transpose(1, 2).reshape(B, q.shape[2], -1)
+        assert rel_err(o.float().cpu().numpy(), want.numpy()) < 2e-2
+
+
+# ----------------------------------------------------------------- CE / embed / pool
+def test_cross_entropy(cuda, golden):
+    K_ = _k()
+    fx = golden("ops")
+    lg = torch.from_numpy(fx["ce:logits"]).to(BF)
+    tg = torch.from_numpy(fx["ce:targets"])
+    out, dl = K_.cross_entropy(lg.to(cuda), tg.to(cuda))
+    ref = O.cross_entropy(lg.float(), tg)
+    assert abs(out[0].item() - float(ref)) / float(ref) < 1e-5
+    p = torch.softmax(lg.float(), -1)
+    oh = torch.zeros_like(p)
+    valid = tg != -100
+    oh[valid, tg[valid]] = 1.0
+    want = torch.where(valid.unsqueeze(1), p - oh, torch.zeros_like(p))
+    assert rel_err(dl.float().cpu().numpy(), want.numpy()) < 8e-3
+    assert abs(out[1].item() - 1.0 / valid.sum().item()) < 1e-7
+    tg2 = torch.from_numpy(fx["ce:targets2"])
+    mk = torch.from_numpy(fx["ce:mask"])
+    out2, _ = K_.cross_entropy(lg.to(cuda), tg2.to(cuda), mask=mk.to(cuda), mask_mode=True)
+    ref2 = O.masked_cross_entropy(lg.float(), tg2, mk)
+    assert abs(out2[0].item() - float(ref2)) / float(ref2) < 1e-5
+
+
+def test_cross_entropy_row_mapping_fullvocab(cuda):
+    """Caption layout: loss rows are logits[:, M:M+T] of a [B, S, V] tensor, V=50304."""
+    K_ = _k()
+    torch.manual_seed(5)
+    B, S, M, T, V = 3, 12, 5, 7, 50304
+    lg = (torch.randn(B, S, V) * 3).to(BF)
+    tg = torch.randint(0, 50257, (B, T))
+    tg[0, 3] = -100
+    out, dl = K_.cross_entropy(lg.view(B * S, V).to(cuda), tg.to(cuda), rows_per_group=T,
+                               group_stride=S, row_offset=M)
+    ref = O.cross_entropy(lg[:, M:M + T].float(), tg)
+    assert abs(out[0].item() - float(ref)) / float(ref) < 1e-5
+
+
+def test_embedding_fwd_bwd(cuda):
+    K_ = _k()
+    torch.manual_seed(7)
+    V, P, C, B, T, M = 300, 64, 128, 3, 20, 4
+    wte = torch.randn(V, C).to(BF)
+    wpe = torch.randn(P, C).to(BF)
+    idx = torch.randint(0, V, (B, T))
+    out = torch.zeros(B, M + T, C, dtype=BF, device=cuda)
+    K_.embedding_fwd(idx.to(cuda), wte.to(cuda), wpe.to(cuda), out, T, M + T, M)
+    want = wte.float()[idx] + wpe.float()[:T]
+    assert rel_err(out[:, M:].float().cpu().numpy(), want.numpy()) < 5e-3
+    assert out[:, :M].abs().max().item() == 0
+    dout = torch.randn(B, M + T, C).to(BF)
+    ate = torch.zeros(V, C, device=cuda)
+    ape = torch.zeros(P, C, device=cuda)
+    K_.embedding_bwd(idx.to(cuda), dout.to(cuda), ate, ape, T, M + T, M, C)
+    wr = wte.float().requires_grad_(True)
+    pr = wpe.float().requires_grad_(True)
+    ((wr[idx] + pr[:T]) * dout[:, M:].float()).sum().backward()
+    assert rel_err(ate.cpu().numpy(), wr.grad.numpy()) < 1e-5
+    assert rel_err(ape.cpu().numpy(), pr.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("side", [16, 14])
+def test_pool_clip(cuda, golden, side):
+    K_ = _k()
+    fx = golden("ops")
+    tok = torch.from_numpy(fx[f"pool{side}:in"])
+    out = K_.pool_clip(tok.to(cuda))
+    assert rel_err(out.cpu().numpy(), fx[f"pool{side}:out"]) < 1e-5
+    outb = K_.pool_clip(tok.to(BF).to(cuda))
+    want = O.pool_clip(tok.to(BF).float())
+    assert rel_err(outb.float().cpu().numpy(), want.numpy()) < 8e-3
+
+
+def test_pool_clip_full_size(cuda):
+    K_ = _k()
+    tok = torch.randn(4, 257, 768)
+    out = K_.pool_clip(tok.to(cuda))
+    assert rel_err(out.cpu().numpy(), O.pool_clip(tok).numpy()) < 1e-5
+
+
+# -------------------------------------------------------------------- optimizer path
+def test_grad_norm_and_adamw(cuda, golden):
+    K_ = _k()
+    fx = golden("ops")
+    p1 = torch.from_numpy(fx["adam:p1"]).to(BF)
+    p2 = torch.from_numpy(fx["adam:p2"]).to(BF)
+    g1 = torch.from_numpy(fx["adam:g1"])
+    g2 = torch.from_numpy(fx["adam:g2"])
+    n1, n2 = p1.numel(), p2.numel()
+    P = torch.cat([p1.reshape(-1), p2.reshape(-1)]).to(cuda)
+    Mm = torch.zeros_like(P)
+    Vv = torch.zeros_like(P)
+    refp = [p1.float().clone(), p2.float().clone()]
+    st = [(torch.zeros_like(refp[0]), torch.zeros_like(refp[0])),
+          (torch.zeros_like(refp[1]), torch.zeros_like(refp[1]))]
+    for it in range(2):
+        gs = [(g1 * (it + 1)).to(BF), (g2 * (it + 1)).to(BF)]
+        G = torch.cat([gs[0].reshape(-1), gs[1].reshape(-1)]).to(cuda)
+        out = K_.grad_norm(G, 1.0)
+        nrm, coef = O.clip_coef([g.float() for g in gs], 1.0)
+        assert abs(out[0].item() - float(nrm)) / float(nrm) < 1e-5
+        assert abs(out[1].item() - coef) < 1e-6
+        K_.adamw(P[:n1], G[:n1], Mm[:n1], Vv[:n1], n1, 1e-3, 0.9, 0.95, 1e-8, 0.1, it + 1, out[1:2])
+        K_.adamw(P[n1:], G[n1:], Mm[n1:], Vv[n1:], n2, 1e-3, 0.9, 0.95, 1e-8, 0.0, it + 1, out[1:2])
+        for j in range(2):
+            O.adamw_update(refp[j], gs[j].float() * coef, st[j][0], st[j][1], it + 1, 1e-3,
+                           wd=0.1 if j == 0 else 0.0)
+    got = P.float().cpu()
+    assert rel_err(got[:n1].numpy(), refp[0].reshape(-1).numpy()) < 1e-2
+    assert rel_err(got[n1:].numpy(), refp[1].reshape(-1).numpy()) < 1e-2
+
+
+def test_colsum_dropout_gate(cuda):
+    K_ = _k()
+    torch.manual_seed(11)
+    x = torch.randn(1000, 96).to(BF)
+    s = K_.colsum(x.to(cuda))
+    assert rel_err(s.float().cpu().numpy(), x.float().sum(0).numpy()) < 8e-3
+    p, seed = 0.1, 77
+    d = K_.dropout_mask_apply(x.to(cuda), p, seed)
+    keep = torch.from_numpy(keep_mask(seed, np.arange(x.numel()), p).reshape(x.shape))
+    want = torch.where(keep, x.float() / (1 - p), torch.zeros_like(x.float()))
+    assert rel_err(d.float().cpu().numpy(), want.numpy()) < 8e-3
+    y = torch.randn(1000, 96).to(BF)
+    gate = torch.tensor(0.3).to(BF)
+    acc = torch.zeros(1, device=cuda)
+    dy = K_.gate_bwd(x.to(cuda), y.to(cuda), gate.to(cuda), acc)
+    t = math.tanh(float(gate.float()))
+    assert rel_err(dy.float().cpu().numpy(), (t * x.float()).numpy()) < 8e-3
+    want_g = (x.float() * y.float()).sum().item() * (1 - t * t)
+    assert abs(acc.item() - want_g) / abs(want_g) < 1e-3
