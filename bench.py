@@ -1,0 +1,298 @@
+"""bench.py — throughput of the MI355X-native GPT-2 hot path (BASELINE.json metric).
+
+Default workload (configs[1]): GPT-2 124M LM pretrain optimizer step, micro-batch 16 x 1024,
+gradient accumulation to 524,288 tokens per step across the job (32 micro-steps at N=1,
+4 per rank at N=8, like train_gpt2.py:244-251), bf16, fused AdamW + clip, RCCL all-reduce.
+A secondary line item times the Q-Former caption step (B=128 per GPU, accumulation 1,
+SURVEY.md D6) — the north star's roofline target.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lm|qformer|linear|cross]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  Inputs are synthetic (random tokens / N(0,1) CLIP tokens),
+resident in HBM before timing; weights random-init with the reference's init recipe.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpt2-vision-language_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (32x32x16 bf16 in 32 cyc) x 2.4 GHz
+PEAK_HBM_GBS = 8000.0
+METRIC = "training tokens/sec/node, GPT-2-124M seq1024; caption-step images/sec"
+# algorithmic work
+LM_FLOP_PER_TOKEN = 798.1e6
+CAP_FLOP_PER_IMAGE = {"qformer": 35.16e9, "linear": 31.98e9, "cross": 21.04e9}
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return world, rank, torch.device(f"cuda:{local}")
+
+
+# --------------------------------------------------------------------------- models
+def build_lm(dev):
+    import gvl.gpt2 as g2
+    torch.manual_seed(0)
+    m = g2.GPT(g2.GPTConfig(vocab_size=50304))
+    return m.to(dev).to(torch.bfloat16)
+
+
+def build_caption(kind, dev):
+    import gvl.caption as cap
+    import gvl.cross_att as xa
+    import gvl.gpt2 as g2
+    torch.manual_seed(0)
+    if kind == "cross":
+        m = xa.GPT(xa.GPTConfig(vocab_size=50304))
+    else:
+        lm = cap.GPT_previous(g2.GPTConfig(vocab_size=50304, block_size=1024))
+        cls = cap.QFormerCaption if kind == "qformer" else cap.LinearCaption
+        m = cls(enc_dim=768, lm=lm, m_vis_tokens=32)
+    return m.to(dev).to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------- workloads
+def run_lm(args, world, rank, dev, timer=None):
+    from gvl.dist import GradBuckets
+    from gvl.optim import get_lr
+    from gvl.train import lm_batch, train_step
+    B, T = args.micro_batch, 1024
+    total = 524288
+    accum = max(1, total // (B * T * world))
+    model = build_lm(dev)
+    model.train()
+    opt = _quiet(lambda: model.configure_optimizers(0.1, 6e-4, "cuda"))
+    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb) if world > 1 else None
+    batches = [lm_batch(B, T, step=i, rank=rank, device=dev) for i in range(accum)]
+    loss_fn = lambda m, b: m(b[0], b[1])[1]
+
+    def step(it):
+        return train_step(model, opt, batches, loss_fn, get_lr(it, 6e-4, 6e-5, 715, 19073),
+                          buckets=buckets)
+
+    tokens_per_step = B * T * accum * world
+    return step, tokens_per_step, dict(workload="gpt2-124m-lm-pretrain", micro_batch=B,
+                                       seq_len=T, grad_accum=accum,
+                                       global_batch=B * accum * world,
+                                       tokens_per_step=tokens_per_step)
+
+
+def run_caption(kind, args, world, rank, dev):
+    from gvl.caption import pool_clip_197_to_33_avg_with_cls as pool
+    from gvl.dist import GradBuckets
+    from gvl.optim import get_lr
+    from gvl.train import caption_batch, caption_labels, train_step
+    B = args.caption_batch
+    model = build_caption(kind, dev)
+    model.train()
+    opt = _quiet(lambda: model.configure_optimizers(0.1, 1e-3, "cuda"))
+    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb) if world > 1 else None
+    z, x, y, m = caption_batch(B, rank=rank, device=dev)
+    if kind == "cross":
+        loss_fn = lambda mm, b: mm(b[1], z=pool(b[0]), targets=b[2], target_mask=b[3])[1]
+    else:
+        lab = caption_labels(y, m)
+        loss_fn = lambda mm, b: mm(pool(b[0]), b[1], labels=lab)[1]
+
+    def step(it):
+        return train_step(model, opt, [(z, x, y, m)], loss_fn, get_lr(it, 1e-3, 1e-4, 5, 80),
+                          buckets=buckets)
+
+    return step, B * world, dict(workload=f"{kind}-caption-step", micro_batch=B, seq_len=31,
+                                 grad_accum=1, global_batch=B * world)
+
+
+def _quiet(fn):
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn()
+
+
+def timed(step, steps, warmup, world, timer=None):
+    from gvl import kernels as K
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if timer is not None:
+        K.set_kernel_timer(timer)
+    t0 = time.perf_counter()
+    r = None
+    for i in range(steps):
+        r = step(warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    K.set_kernel_timer(None)
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    return dt, r
+
+
+def dominant_kernel(summary):
+    name, s = max(summary.items(), key=lambda kv: kv[1]["ms"])
+    avg_ms = s["ms"] / s["launches"]
+    achieved = s["flops"] / (s["ms"] * 1e-3) / 1e12
+    return dict(kernel=name, bound="mfma", achieved=round(achieved, 1), peak=PEAK_BF16_TFLOPS,
+                unit="TFLOP/s", frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None,
+                launches=s["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
+                avg_flop_per_launch=s["flops"] / s["launches"],
+                all_gemm_frac=round(sum(v["flops"] for v in summary.values())
+                                    / (sum(v["ms"] for v in summary.values()) * 1e-3) / 1e12
+                                    / PEAK_BF16_TFLOPS, 4))
+
+
+# ---------------------------------------------------------------------- CPU baseline
+def cpu_baseline(workload, seconds=15.0):
+    """The oracle (fp32 CPU restatement of the reference step) on this host's cores:
+    zero_grad -> fwd -> bwd -> clip -> AdamW on a bounded sample (LM: B=1 x 1024 tokens;
+    caption: B=8 images), repeated until ~`seconds` of CPU work."""
+    from oracle import models as OM
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    import gvl.gpt2 as g2
+    with torch.device("meta"):
+        if workload == "lm":
+            mdl = g2.GPT(g2.GPTConfig(vocab_size=50304))
+        else:
+            mdl = build_caption_meta(workload)
+    keys = [(k, tuple(v.shape)) for k, v in mdl.state_dict().items() if not k.endswith("attn.bias")]
+    g = torch.Generator().manual_seed(0)
+    P = {k: torch.randn(s, generator=g) * 0.02 for k, s in keys}
+    if workload == "lm":
+        P["transformer.wte.weight"] = P["lm_head.weight"]
+        ids = torch.randint(0, 50257, (1, 1025), generator=g)
+        x, y = ids[:, :-1], ids[:, 1:]
+        kind, units_per_step, unit = "gpt", 1024, "tokens/s"
+        train = OM.trainable_keys("gpt", list(P))
+        loss_of = lambda P_, it: OM.gpt_forward(P_, x, 12, 12, y)[1]
+        sample = "GPT-2 124M LM step, B=1 x T=1024 (fp32, oracle restatement)"
+    else:
+        from gvl.train import caption_batch, caption_labels
+        from oracle import ops as O
+        z, xx, yy, mm = caption_batch(8, device="cpu")
+        zp = O.pool_clip(z)
+        lab = caption_labels(yy, mm)
+        P["gpt.transformer.wte.weight"] = P["gpt.lm_head.weight"]
+        kind = {"qformer": "qformer", "linear": "linear"}.get(workload, "cross")
+        units_per_step, unit = 8, "images/s"
+        train = OM.trainable_keys(kind, list(P))
+        if kind == "cross":
+            loss_of = lambda P_, it: OM.cross_att_forward(P_, xx, zp, 12, 12, yy, mm)[1]
+        else:
+            loss_of = lambda P_, it: OM.caption_forward(P_, kind, zp, xx, 12, 12, 1024, lab)[1]
+        sample = f"{workload} caption step, B=8 images (fp32, oracle restatement)"
+    OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 20:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(units_per_step * n / dt, 2), unit=unit, cores=threads, kind="port",
+                sample=f"{sample}; {n} steps in {dt:.1f}s")
+
+
+def build_caption_meta(kind):
+    import gvl.caption as cap
+    import gvl.cross_att as xa
+    import gvl.gpt2 as g2
+    if kind == "cross":
+        return xa.GPT(xa.GPTConfig(vocab_size=50304))
+    lm = cap.GPT_previous(g2.GPTConfig(vocab_size=50304, block_size=1024))
+    cls = cap.QFormerCaption if kind == "qformer" else cap.LinearCaption
+    return cls(enc_dim=768, lm=lm, m_vis_tokens=32)
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="lm", choices=["lm", "qformer", "linear", "cross"])
+    ap.add_argument("--micro-batch", type=int, default=16)
+    ap.add_argument("--caption-batch", type=int, default=128)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--caption-steps", type=int, default=10)
+    args = ap.parse_args()
+
+    world, rank, dev = setup()
+    from gvl import _lib
+    from gvl import kernels as K
+    _lib.load()
+
+    if args.workload == "lm":
+        step, units, cfg = run_lm(args, world, rank, dev)
+        unit, flop_per_unit = "tokens/s", LM_FLOP_PER_TOKEN
+    else:
+        step, units, cfg = run_caption(args.workload, args, world, rank, dev)
+        unit, flop_per_unit = "images/s", CAP_FLOP_PER_IMAGE[args.workload]
+    timer = K.KernelTimer()
+    dt, res = timed(step, args.steps, args.warmup, world, timer)
+    value = units * args.steps / dt
+    roof = dominant_kernel(timer.summary())
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "strong" if args.workload == "lm" else "weak", "vs_baseline": None,
+        "dtype": "bf16", "data": "synthetic (random tokens / N(0,1) CLIP tokens), random-init weights",
+        "config": dict(cfg, model="gpt2-124m", parallelism=f"dp{world}"),
+        "step_mfma_frac": round(value * flop_per_unit / 1e12 / PEAK_BF16_TFLOPS / world, 4),
+        "loss": round(float(res.loss), 5), "grad_norm": round(float(res.norm), 5),
+        "roofline": roof,
+    }
+    if args.workload == "lm" and not args.no_secondary:
+        del step
+        torch.cuda.empty_cache()
+        cstep, cunits, ccfg = run_caption("qformer", args, world, rank, dev)
+        ctimer = K.KernelTimer()
+        cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer)
+        cval = cunits * args.caption_steps / cdt
+        out["caption_qformer"] = dict(
+            value=round(cval, 1), unit="images/s", ms_per_step=round(cdt / args.caption_steps * 1e3, 3),
+            step_mfma_frac=round(cval * CAP_FLOP_PER_IMAGE["qformer"] / 1e12 / PEAK_BF16_TFLOPS / world, 4),
+            loss=round(float(cres.loss), 5), config=ccfg, roofline=dominant_kernel(ctimer.summary()))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

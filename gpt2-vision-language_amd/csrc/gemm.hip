@@ -231,7 +231,9 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GVL_REQUIRE(d->m >= 0 && d->n >= 0 && d->k >= 0, "gvl_gemm: negative size");
   if (d->m == 0 || d->n == 0) return 0;
   GVL_REQUIRE(d->a && d->b && d->c, "gvl_gemm: null operand");
-  GVL_REQUIRE(d->k % 8 == 0, "gvl_gemm: K=%lld must be a multiple of 8", (long long)d->k);
+  // 16-B vector loads run along K only for K-contiguous operands
+  GVL_REQUIRE((d->a_mn && d->b_mn) || d->k % 8 == 0,
+              "gvl_gemm: K=%lld must be a multiple of 8", (long long)d->k);
   GVL_REQUIRE(d->n % 4 == 0, "gvl_gemm: N=%lld must be a multiple of 4", (long long)d->n);
   GVL_REQUIRE(!d->a_mn || d->m % 8 == 0, "gvl_gemm: M must be a multiple of 8 for MN-major A");
   GVL_REQUIRE(!d->b_mn || d->n % 8 == 0, "gvl_gemm: N must be a multiple of 8 for MN-major B");

@@ -60,7 +60,7 @@ class GPTBlockFn(torch.autograd.Function):
         hpre = torch.empty(B * T, fc_w.shape[0], dtype=BF16, device=x.device)
         h = K.linear(xn2, fc_w, fc_b, act=1, pre_out=hpre)
         out = K.linear(h, mproj_w, mproj_b, residual=xm)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, xn1, m1, r1, qkv, y, lse, xm, xn2, m2, r2, hpre, h, ln1_w,
                                   attn_w, aproj_w, ln2_w, fc_w, mproj_w)
             ctx.shape = (B, T, C, n_head, causal)
@@ -126,7 +126,7 @@ class LayerNormFn(torch.autograd.Function):
             x2 = x2.to(BF16)
         x2 = x2.contiguous()
         y, mean, rstd = K.layernorm_fwd(x2, w, b, eps)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w, mean, rstd)
             ctx.shp = shp
         return y.view(shp)
@@ -166,7 +166,7 @@ class LinearFn(torch.autograd.Function):
         if gate is not None:
             ybr = torch.empty(x2.shape[0], N, dtype=BF16, device=x.device)
         y = K.linear(x2, w, b, residual=r2, gate=gate, pre_out=ybr, drop_p=drop_p, seed=seed)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w, gate, ybr)
             ctx.cfg = (shp, N, drop_p, seed, residual is not None)
         return y.view(*shp[:-1], N)
@@ -207,7 +207,7 @@ class MLPFn(torch.autograd.Function):
         h = K.linear(x2, w1, b1, act=act, pre_out=hpre)
         r2 = residual.reshape(-1, w2.shape[0]).to(BF16).contiguous() if residual is not None else None
         y = K.linear(h, w2, b2, residual=r2, drop_p=drop_p, seed=seed)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w1, w2, hpre, h)
             ctx.cfg = (shp, act, drop_p, seed, residual is not None)
         return y.view(*shp[:-1], w2.shape[0])
@@ -263,7 +263,7 @@ class MHAFn(torch.autograd.Function):
         o, lse = K.attn_fwd(qv, kv_, vv, n_head, False, drop_p=p_attn, seed=sa)
         r2 = residual.reshape(B * Tq, C).to(BF16).contiguous()
         out = K.linear(o.view(B * Tq, C), out_w, out_b, residual=r2, drop_p=p_out, seed=seed)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse)
             ctx.cfg = (B, Tq, Tk, C, n_head, self_attn, p_attn, p_out, seed, sa)
         return out.view(B, Tq, C)
@@ -332,7 +332,7 @@ class CrossAttnFn(torch.autograd.Function):
         o, lse = K.attn_fwd(qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], n_head, False)
         ybr = torch.empty(B * T, C, dtype=BF16, device=x.device)
         out = K.linear(o.view(B * T, C), c_w, c_b, residual=x2, gate=gate, pre_out=ybr)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w,
                                   c_w, gate)
             ctx.cfg = (B, T, S, C, n_head)
@@ -395,7 +395,7 @@ class EmbedFn(torch.autograd.Function):
         if prefix is not None:
             out[:, :M].copy_(prefix)
         K.embedding_fwd(idx, wte, wpe, out, T, S, M)
-        if torch.is_grad_enabled():
+        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(idx)
             ctx.cfg = (B, T, C, M, S, wte.shape[0], wpe.shape[0], wte.dtype, wpe.dtype)
         return out
@@ -435,7 +435,7 @@ class LMHeadLossFn(torch.autograd.Function):
         x2 = x.reshape(B * S, C).to(BF16).contiguous()
         logits = K.linear(x2, w)
         V = w.shape[0]
-        need = torch.is_grad_enabled() and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         out, dl = K.cross_entropy(logits, targets, rows_per_group=T, group_stride=S,
                                   row_offset=row_offset, mask=mask, mask_mode=mask_mode,
                                   want_grad=need)

@@ -44,6 +44,37 @@ def _rowmajor(t, name):
                          f"strides {t.stride()})")
 
 
+# ------------------------------------------------------------------ live kernel timing
+class KernelTimer:
+    """Brackets every GEMM launch with HIP events on the launch stream (bench.py uses it
+    over its timed region to report the dominant kernel's achieved TFLOP/s)."""
+
+    def __init__(self):
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, flops in self.records:
+            s = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            s["launches"] += 1
+            s["ms"] += e0.elapsed_time(e1)
+            s["flops"] += flops
+        return out
+
+
+_timer = None
+
+
+def set_kernel_timer(t):
+    global _timer
+    _timer = t
+
+
+GEMM_NAMES = {(0, 0): "gemm_bf16_kernel<false,false>", (0, 1): "gemm_bf16_kernel<false,true>",
+              (1, 0): "gemm_bf16_kernel<true,false>", (1, 1): "gemm_bf16_kernel<true,true>"}
+
+
 # ------------------------------------------------------------------------------- GEMM
 def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, bias=None,
          act=0, dact=0, pre_out=None, pre_in=None, residual=None, gate=None, drop_p=0.0,
@@ -81,6 +112,14 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     d.drop_p = float(drop_p)
     d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     d.c_fp32 = int(out.dtype == F32)
+    if _timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
+        e1.record()
+        _timer.records.append((GEMM_NAMES[(int(a_mn), int(b_mn))], e0, e1, 2.0 * M * N * K))
+        return out
     _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
     return out
 

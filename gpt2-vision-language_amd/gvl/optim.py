@@ -160,6 +160,8 @@ def clip_grad_norm_(optimizer_or_params, max_norm: float):
     utility on the given parameters (eager, not the hot path)."""
     if isinstance(optimizer_or_params, AdamW):
         return optimizer_or_params.clip_grad_norm_(max_norm)
+    if isinstance(optimizer_or_params, torch.optim.Optimizer):
+        optimizer_or_params = [p for g in optimizer_or_params.param_groups for p in g["params"]]
     return torch.nn.utils.clip_grad_norm_(optimizer_or_params, max_norm)
 
 
