@@ -1,6 +1,7 @@
-// bf16 GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_bf16) with a fused epilogue.
+// bf16 GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_bf16) with a fused epilogue — entry point
+// and the register-staged fallback kernel (any K % 8 == 0, tails in every dimension).
 //
-// Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave a 64x64 sub-tile of
+// Fallback tile 128x128x64, 256 threads = 4 waves in 2x2, each wave a 64x64 sub-tile of
 // 4x4 MFMA tiles.  Operands are register-staged through a double-buffered LDS image:
 //   K-contiguous operand  -> [128 rows][64 k]   128-B rows, 16-B chunk XOR (row>>1)&7,
 //                            fragments by ds_read_b128 (conflict-free for 16x16x32 maps);
@@ -9,35 +10,18 @@
 // The MFMA is issued with operands swapped (B-fragment as "A") so each lane owns one
 // output row and four consecutive output columns -> 8-byte epilogue stores.
 // Workgroups are remapped so that consecutive tiles share an XCD (L2) — T1 of the guide.
+// The fast path (gemm_lds.hip: LDS-DMA staging, 256-wide tiles) is used whenever K % 64 == 0.
+#include <stdlib.h>
+
 #include "common.h"
 #include "capi_util.h"
+#include "gemm_common.h"
 #include "../../include/gvl.h"
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int STAGE_BYTES = 2 * 16384;  // A image + B image
-
-struct GemmP {
-  const bf16_t* A;
-  const bf16_t* B;
-  void* C;
-  int64_t M, N, K, lda, ldb, ldc;
-  float alpha;
-  const float* alpha_ptr;
-  const bf16_t* bias;
-  bf16_t* pre_out;
-  const bf16_t* pre_in;
-  int64_t ldp;
-  const bf16_t* residual;
-  int64_t ldr;
-  const bf16_t* gate;
-  uint64_t seed;
-  float drop_scale;
-  uint32_t drop_thresh;
-  int tiles_m, tiles_n;
-  int act, dact, c_f32, has_drop;
-};
 
 GVL_DEV int swz_k(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 GVL_DEV int fT(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
@@ -161,70 +145,32 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
     }
     __syncthreads();
   }
+  gemm_epilogue<4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
+}
 
-  // ---- epilogue: lane owns row m, columns n..n+3 of each 16x16 tile ----
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  const float gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= p.N) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
-      if (p.bias) {
-        const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
-        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
-      }
-      if (p.dact) {
-        const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
-        const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
-      }
-      if (p.act) {
-        if (p.pre_out) {
-          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
-      }
-      if (p.has_drop) {
-        const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = rng_keep(p.seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
-      }
-      if (p.gate) {
-        if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient
-          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= gatev;
-      }
-      if (p.residual) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
-        v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
-      }
-      if (p.c_f32) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + m * p.ldc + n) =
-            make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
+// GVL_GEMM_IMPL=regstage forces the fallback; GVL_GEMM_CFG=0|1|2 forces a tile config.
+struct GemmEnv {
+  int impl = 1, cfg = -1;
+  GemmEnv() {
+    const char* s = getenv("GVL_GEMM_IMPL");
+    if (s && s[0] == 'r') impl = 0;
+    const char* c = getenv("GVL_GEMM_CFG");
+    if (c) cfg = atoi(c);
   }
+};
+GemmEnv& env() {
+  static GemmEnv e;
+  return e;
 }
 
 }  // namespace
+
+extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
+  GVL_REQUIRE(impl >= 0 && impl <= 1 && cfg >= -1 && cfg <= 2, "gvl_gemm_tune: bad arguments");
+  env().impl = impl;
+  env().cfg = cfg;
+  return 0;
+}
 
 extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GVL_REQUIRE(d != nullptr, "gvl_gemm: null descriptor");
@@ -265,10 +211,21 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
+  p.splits = 1;
+  p.kper = d->k;
+  p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
+             ? static_cast<float*>(d->workspace) : nullptr;
+  p.ws_bytes = p.ws ? d->workspace_bytes : 0;
+  hipStream_t s = gvl::as_stream(stream);
+  if (env().impl == 1 && gvl::gemm_lds_ok(d)) {
+    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg);
+    gvl::gemm_lds_launch(p, d->a_mn, d->b_mn, cfg, s);
+    GVL_LAUNCH_CHECK("gvl_gemm(lds)");
+    return 0;
+  }
   p.tiles_m = (int)((d->m + BM - 1) / BM);
   p.tiles_n = (int)((d->n + BN - 1) / BN);
   const int grid = p.tiles_m * p.tiles_n;
-  hipStream_t s = gvl::as_stream(stream);
   if (!d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, false>), dim3(grid), dim3(NT), 0, s, p);
   else if (!d->a_mn && d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, true>), dim3(grid), dim3(NT), 0, s, p);
   else if (d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<true, false>), dim3(grid), dim3(NT), 0, s, p);

@@ -1,0 +1,146 @@
+// Shared GEMM parameter block and fused epilogue (gemm.hip, gemm_lds.hip).
+#pragma once
+#include "common.h"
+#include "../../include/gvl.h"
+
+struct GemmP {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  int64_t M, N, K, lda, ldb, ldc;
+  float alpha;
+  const float* alpha_ptr;
+  const bf16_t* bias;
+  bf16_t* pre_out;
+  const bf16_t* pre_in;
+  int64_t ldp;
+  const bf16_t* residual;
+  int64_t ldr;
+  const bf16_t* gate;
+  uint64_t seed;
+  float drop_scale;
+  uint32_t drop_thresh;
+  int tiles_m, tiles_n;
+  int act, dact, c_f32, has_drop;
+  // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
+  // writing fp32 partials to ws[s][M][N]; gemm_splitk_reduce applies the epilogue.
+  int splits;
+  int64_t kper;
+  float* ws;
+  int64_t ws_bytes;
+};
+
+// Epilogue for accumulators produced with swapped operands: acc[i][j] holds, for this lane,
+// row m = mw0 + 16 i + (lane & 15) and columns n = nw0 + 16 j + 4 (lane >> 4) + r, r = 0..3.
+// Order: *alpha(*alpha_ptr), +bias, *dgelu(pre_in), {pre_out; gelu}, dropout,
+// {pre_out if gate && !act; *tanh(gate)}, +residual, store bf16|fp32.
+// One 4-column group of one row.  The tile loops around it must unroll completely or the
+// accumulator array is demoted to scratch: the Makefile raises -pragma-unroll-threshold.
+static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a, int64_t m,
+                                                        int64_t n, float alpha, float gatev);
+
+template <int FM, int FN>
+GVL_DEV void gemm_epilogue(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
+                           int64_t nw0, int lane) {
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
+  const bool plain = !p.bias && !p.dact && !p.act && !p.has_drop && !p.gate && !p.residual &&
+                     !p.c_f32;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t m = mw0 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t n = nw0 + j * 16 + 4 * (lane >> 4);
+      if (m < p.M && n < p.N) {
+        if (plain) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+              make_uint2(pack2(acc[i][j][0] * alpha, acc[i][j][1] * alpha),
+                         pack2(acc[i][j][2] * alpha, acc[i][j][3] * alpha));
+        } else {
+          gemm_epi_quad(p, acc[i][j], m, n, alpha, gatev);
+        }
+      }
+    }
+  }
+}
+
+static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a, int64_t m,
+                                                        int64_t n, float alpha, float gatev) {
+  {
+    {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
+      if (p.bias) {
+        const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
+        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+      }
+      if (p.dact) {
+        const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
+        const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+      }
+      if (p.act) {
+        if (p.pre_out) {
+          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
+      }
+      if (p.has_drop) {
+        const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = rng_keep(p.seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
+      }
+      if (p.gate) {
+        if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient
+          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= gatev;
+      }
+      if (p.residual) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
+        v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+      }
+      if (p.c_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + m * p.ldc + n) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// Store raw fp32 accumulators of a split-K slice.
+template <int FM, int FN>
+GVL_DEV void gemm_store_partial(const GemmP& p, const float4_t (&acc)[FM][FN], int split,
+                                int64_t mw0, int64_t nw0, int lane) {
+  float* base = p.ws + (int64_t)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t m = mw0 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t n = nw0 + j * 16 + 4 * (lane >> 4);
+      if (m < p.M && n < p.N)
+        *reinterpret_cast<float4*>(base + m * p.N + n) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+}
+
+namespace gvl {
+int gemm_lds_pick(int64_t M, int64_t N, int64_t K, int forced);
+int gemm_splitk_pick(int64_t tiles, int64_t K);
+bool gemm_lds_ok(const gvl_gemm_desc* d);
+int gemm_lds_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
+}  // namespace gvl

@@ -163,16 +163,32 @@ __global__ __launch_bounds__(LN_NT) void ln_bwd_kernel(
   }
 }
 
-__global__ void ln_bwd_finalize(const float* __restrict__ ws, int nblk, int C,
-                                bf16_t* __restrict__ dw, bf16_t* __restrict__ db, int acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
-  float s = 0.f;
-  for (int k = 0; k < nblk; ++k) s += ws[(int64_t)k * 2 * C + c];
+// Column reduction of the per-block partials: block = 64 columns x 4 partial-groups, each
+// thread summing nblk/4 partials with 8 independent loads in flight (the partials were
+// previously summed by one serial dependent-load chain per column: ~120 us).
+__global__ __launch_bounds__(256) void ln_bwd_finalize(const float* __restrict__ ws, int nblk,
+                                                       int C, bf16_t* __restrict__ dw,
+                                                       bf16_t* __restrict__ db, int acc) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < 2 * C) {
+    int k = g;
+    for (; k + 28 < nblk; k += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += ws[(int64_t)(k + 4 * j) * 2 * C + c];
+    }
+    for (; k < nblk; k += 4) s[0] += ws[(int64_t)k * 2 * C + c];
+  }
+  red[g][cl] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (g != 0 || c >= 2 * C) return;
+  float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
   bf16_t* dst = (c < C) ? (dw ? dw + c : nullptr) : (db ? db + (c - C) : nullptr);
   if (!dst) return;
-  if (acc) s += bf2f(*dst);
-  *dst = f2bf(s);
+  if (acc) t += bf2f(*dst);
+  *dst = f2bf(t);
 }
 
 int ln_bwd_blocks(int64_t rows) {
@@ -220,7 +236,7 @@ extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
                      rstd, static_cast<bf16_t*>(dx), lddx, (int)accumulate_dx, ws, rows, (int)cols);
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd");
   if (ws) {
-    const int g2 = (int)((2 * cols + 255) / 256);
+    const int g2 = (int)((2 * cols + 63) / 64);
     hipLaunchKernelGGL(ln_bwd_finalize, dim3(g2), dim3(256), 0, s, ws, nb, (int)cols,
                        static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), (int)accumulate_wb);
     GVL_LAUNCH_CHECK("gvl_layernorm_bwd(finalize)");

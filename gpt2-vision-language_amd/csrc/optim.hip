@@ -109,22 +109,44 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ p,
   }
 }
 
-// Column sums: block b sums rows [b*chunk, (b+1)*chunk) for all columns -> ws[b][cols].
+// Column sums (bias gradients).  Block (cx, s): 64 column-threads x 8 columns (16-B loads,
+// one 1-KiB coalesced row segment per wave) x 4 row groups, over rows [s*chunk, (s+1)*chunk),
+// 4 rows in flight per thread; the 4 row groups reduce through LDS into ws[s][cols].
+constexpr int CS_SPLITS = 64;
+
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ x,
                                                              int64_t rows, int64_t cols, int64_t ld,
                                                              int64_t chunk, float* __restrict__ ws) {
-  const int64_t r0 = (int64_t)blockIdx.x * chunk;
-  int64_t r1 = r0 + chunk;
-  if (r1 > rows) r1 = rows;
-  for (int64_t c = threadIdx.x * 2; c < cols; c += 512) {
-    float s0 = 0.f, s1 = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(x + r * ld + c);
-      s0 += lo_bf(u);
-      s1 += hi_bf(u);
+  __shared__ float red[4][512];
+  const int ct = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 512 + ct * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      uint4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = *reinterpret_cast<const uint4*>(x + (r + 4 * k) * ld + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[0] += lo_bf(u[k].x); s[1] += hi_bf(u[k].x); s[2] += lo_bf(u[k].y); s[3] += hi_bf(u[k].y);
+        s[4] += lo_bf(u[k].z); s[5] += hi_bf(u[k].z); s[6] += lo_bf(u[k].w); s[7] += hi_bf(u[k].w);
+      }
     }
-    ws[(int64_t)blockIdx.x * cols + c] = s0;
-    ws[(int64_t)blockIdx.x * cols + c + 1] = s1;
+    for (; r < r1; r += 4) {
+      const uint4 u = *reinterpret_cast<const uint4*>(x + r * ld + c);
+      s[0] += lo_bf(u.x); s[1] += hi_bf(u.x); s[2] += lo_bf(u.y); s[3] += hi_bf(u.y);
+      s[4] += lo_bf(u.z); s[5] += hi_bf(u.z); s[6] += lo_bf(u.w); s[7] += hi_bf(u.w);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][ct * 8 + k] = s[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int64_t cc = (int64_t)blockIdx.x * 512 + i;
+    if (cc < cols) ws[(int64_t)blockIdx.y * cols + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
   }
 }
 
@@ -132,15 +154,21 @@ __global__ void colsum_finish_kernel(const float* __restrict__ ws, int nb, int64
                                      bf16_t* __restrict__ out, int acc) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cols) return;
-  float s = 0.f;
-  for (int k = 0; k < nb; ++k) s += ws[(int64_t)k * cols + c];
-  if (acc) s += bf2f(out[c]);
-  out[c] = f2bf(s);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= nb; k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += ws[(int64_t)(k + j) * cols + c];
+  }
+  for (; k < nb; ++k) s[0] += ws[(int64_t)k * cols + c];
+  float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  if (acc) t += bf2f(out[c]);
+  out[c] = f2bf(t);
 }
 
 int colsum_blocks(int64_t rows, int64_t* chunk) {
-  int64_t nb = (rows + 63) / 64;
-  if (nb > 256) nb = 256;
+  int64_t nb = (rows + 127) / 128;
+  if (nb > CS_SPLITS) nb = CS_SPLITS;
   if (nb < 1) nb = 1;
   *chunk = (rows + nb - 1) / nb;
   return (int)nb;
@@ -255,8 +283,9 @@ extern "C" int64_t gvl_colsum_workspace_size(int64_t rows, int64_t cols) {
 
 extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
                           int32_t accumulate, void* workspace, gvl_stream_t stream) {
-  GVL_REQUIRE(cols % 2 == 0 && ld % 2 == 0, "gvl_colsum: cols/ld must be even");
+  GVL_REQUIRE(cols % 8 == 0 && ld % 8 == 0, "gvl_colsum: cols/ld must be multiples of 8");
   GVL_REQUIRE(workspace && out, "gvl_colsum: null buffer");
+  GVL_REQUIRE(rows == 0 || gvl::aligned16(x), "gvl_colsum: x must be 16-byte aligned");
   if (cols == 0) return 0;
   int64_t chunk;
   const int nb = colsum_blocks(rows, &chunk);
@@ -264,7 +293,7 @@ extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld,
   if (rows == 0) {
     (void)hipMemsetAsync(workspace, 0, cols * sizeof(float), s);
   } else {
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, s,
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols + 511) / 512), nb), dim3(256), 0, s,
                        static_cast<const bf16_t*>(x), rows, cols, ld, chunk,
                        static_cast<float*>(workspace));
     GVL_LAUNCH_CHECK("gvl_colsum(partial)");

@@ -34,6 +34,7 @@ class GemmDesc(C.Structure):
         ("gate", c_vp),
         ("drop_p", c_f32), ("seed", c_u64),
         ("c_fp32", c_i32),
+        ("workspace", c_vp), ("workspace_bytes", c_i64),
     ]
 
 
@@ -64,6 +65,7 @@ SIGNATURES = {
     "gvl_last_error": (C.c_char_p, []),
     "gvl_abi_version": (C.c_int, []),
     "gvl_gemm": (C.c_int, [C.POINTER(GemmDesc), c_vp]),
+    "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
     "gvl_layernorm_fwd": (C.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                     c_i64, c_i64, c_f32, c_vp]),
     "gvl_layernorm_bwd_workspace_size": (c_i64, [c_i64, c_i64]),

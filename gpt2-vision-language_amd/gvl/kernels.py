@@ -75,6 +75,21 @@ GEMM_NAMES = {(0, 0): "gemm_bf16_kernel<false,false>", (0, 1): "gemm_bf16_kernel
               (1, 0): "gemm_bf16_kernel<true,false>", (1, 1): "gemm_bf16_kernel<true,true>"}
 
 
+_WS = {}
+GEMM_WORKSPACE_MB = 64
+
+
+def _gemm_workspace(device):
+    """Per-device fp32 split-K scratch, allocated once (stream-ordered reuse; allocate it
+    before any hipGraph capture — bench/train warm up eagerly first)."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.empty(GEMM_WORKSPACE_MB * 1024 * 1024 // 4, dtype=F32, device=device)
+        _WS[key] = ws
+    return ws
+
+
 # ------------------------------------------------------------------------------- GEMM
 def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, bias=None,
          act=0, dact=0, pre_out=None, pre_in=None, residual=None, gate=None, drop_p=0.0,
@@ -112,6 +127,8 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     d.drop_p = float(drop_p)
     d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     d.c_fp32 = int(out.dtype == F32)
+    ws = _gemm_workspace(a.device)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
     if _timer is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

@@ -65,8 +65,14 @@ typedef struct gvl_gemm_desc {
   float drop_p;           /* dropout probability on the branch (0 = off) */
   uint64_t seed;
   int32_t c_fp32;         /* 1: C is fp32 */
+  void* workspace;        /* optional fp32 scratch for split-K (few output tiles, long K) */
+  int64_t workspace_bytes;
 } gvl_gemm_desc;
 int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
+/* Process-wide GEMM implementation knob (benchmarking / A-B tests): impl 1 = LDS-DMA
+ * kernel when K % 64 == 0 (default), 0 = register-staged kernel always; cfg -1 = pick
+ * the tile by shape, 0/1/2 = force 256x256 / 256x128 / 128x128. */
+int gvl_gemm_tune(int32_t impl, int32_t cfg);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (eps given; reference uses 1e-5).

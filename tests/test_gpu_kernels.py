@@ -56,6 +56,25 @@ def test_gemm_layouts(cuda, a_mn, b_mn, M, N, K):
     assert rel_err(c.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
+                                             (0, 0, 384, 256, 6144)])
+def test_gemm_splitk_epilogue(cuda, a_mn, b_mn, M, N, K):
+    """Few output tiles + long K -> split-K partials + reduce kernel applying the epilogue."""
+    K_ = _k()
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    alpha = torch.tensor([0.5], dtype=torch.float32)
+    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), bias=bias.to(cuda), act=1,
+                residual=res.to(cuda), alpha_ptr=alpha.to(cuda))
+    ref = O.gelu_tanh(0.5 * (a.float() @ b.float()) + bias.float()) + res.float()
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("act", [1, 2])
 def test_gemm_epilogue_act_bias_residual(cuda, act):
     K_ = _k()

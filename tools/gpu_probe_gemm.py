@@ -1,107 +1,89 @@
-"""Early GPU probe: gvl_gemm layouts/epilogues vs torch fp32, plus a timing sweep.
-
-Run on the GPU box: python tools/gpu_probe_gemm.py
-"""
-import ctypes as C
+"""GPU probe: GEMM implementations/tile configs — correctness (all layouts) and timing
+against torch.mm (hipBLASLt) on the hot-path shapes.  python tools/gpu_probe_gemm.py"""
 import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "gpt2-vision-language_amd"))
-from gvl._lib import GemmDesc  # noqa: E402
+from gvl import _lib  # noqa: E402
+from gvl import kernels as K  # noqa: E402
 
-lib = C.CDLL(os.path.join(os.path.dirname(__file__), "..", "gpt2-vision-language_amd", "gvl", "libgvl.so"))
-lib.gvl_gemm.argtypes = [C.POINTER(GemmDesc), C.c_void_p]
-lib.gvl_last_error.restype = C.c_char_p
-
-
-def gemm(A, B, M, N, K, a_mn, b_mn, bias=None, act=0, residual=None, c=None):
-    if c is None:
-        c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-    d = GemmDesc()
-    d.a, d.b, d.c = A.data_ptr(), B.data_ptr(), c.data_ptr()
-    d.m, d.n, d.k = M, N, K
-    d.lda, d.ldb, d.ldc = A.stride(0), B.stride(0), c.stride(0)
-    d.a_mn, d.b_mn = a_mn, b_mn
-    d.alpha = 1.0
-    d.bias = bias.data_ptr() if bias is not None else None
-    d.act = act
-    d.residual = residual.data_ptr() if residual is not None else None
-    d.ldr = residual.stride(0) if residual is not None else 0
-    rc = lib.gvl_gemm(C.byref(d), C.c_void_p(torch.cuda.current_stream().cuda_stream))
-    assert rc == 0, lib.gvl_last_error()
-    return c
+L = _lib.load()
+IMPLS = [("regstage", 0, -1), ("lds256x256", 1, 0), ("lds256x128", 1, 1), ("lds128x128", 1, 2),
+         ("lds-auto", 1, -1)]
 
 
-def check(M, N, K, a_mn, b_mn, **kw):
-    torch.manual_seed(0)
-    a = torch.randn(M, K, device="cuda").bfloat16()
-    b = torch.randn(K, N, device="cuda").bfloat16()
-    A = a.t().contiguous() if a_mn else a.contiguous()      # a_mn: stored [K][M]
-    B = b.contiguous() if b_mn else b.t().contiguous()      # b_mn: stored [K][N] else [N][K]
-    bias = torch.randn(N, device="cuda").bfloat16() if kw.get("bias") else None
-    res = torch.randn(M, N, device="cuda").bfloat16() if kw.get("res") else None
-    act = kw.get("act", 0)
-    c = gemm(A, B, M, N, K, a_mn, b_mn, bias=bias, act=act, residual=res)
-    ref = a.float() @ b.float()
-    if bias is not None:
-        ref = ref + bias.float()
-    if act == 1:
-        ref = torch.nn.functional.gelu(ref, approximate="tanh")
-    if act == 2:
-        ref = torch.nn.functional.gelu(ref)
-    if res is not None:
-        ref = ref + res.float()
-    torch.cuda.synchronize()
-    err = (c.float() - ref).abs().max().item()
-    rel = err / ref.abs().max().item()
-    print(f"M={M} N={N} K={K} a_mn={a_mn} b_mn={b_mn} {kw} maxabs={err:.4g} rel={rel:.3g}", flush=True)
-    return rel
+def mk(M, N, Kd, a_mn, b_mn, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = torch.randn(M, Kd, device="cuda", generator=g).bfloat16()
+    b = torch.randn(Kd, N, device="cuda", generator=g).bfloat16()
+    A = a.t().contiguous() if a_mn else a
+    B = b.contiguous() if b_mn else b.t().contiguous()
+    return a, b, A, B
 
 
-def bench(M, N, K, a_mn, b_mn, iters=20):
-    a = torch.randn(K if a_mn else M, M if a_mn else K, device="cuda").bfloat16()
-    b = torch.randn(K if b_mn else N, N if b_mn else K, device="cuda").bfloat16()
-    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+def check():
+    worst = 0.0
+    for name, impl, cfg in IMPLS:
+        L.gvl_gemm_tune(impl, cfg)
+        for (M, N, Kd) in [(256, 256, 128), (200, 136, 192), (520, 264, 256), (64, 8, 64)]:
+            for am, bm in [(0, 0), (0, 1), (1, 0), (1, 1)]:
+                if (am and M % 8) or (bm and N % 8):
+                    continue
+                a, b, A, B = mk(M, N, Kd, am, bm, M + N)
+                bias = torch.randn(N, device="cuda").bfloat16()
+                res = torch.randn(M, N, device="cuda").bfloat16()
+                c = K.gemm(A, B, a_mn=bool(am), b_mn=bool(bm), bias=bias, act=1, residual=res)
+                ref = torch.nn.functional.gelu(a.float() @ b.float() + bias.float(),
+                                               approximate="tanh") + res.float()
+                rel = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+                worst = max(worst, rel)
+                if rel > 1e-2:
+                    print(f"FAIL {name} M={M} N={N} K={Kd} a_mn={am} b_mn={bm} rel={rel:.3g}",
+                          flush=True)
+    L.gvl_gemm_tune(1, -1)
+    print("CHECK worst rel", worst, flush=True)
+    return worst
+
+
+def timeit(fn, iters=20):
     for _ in range(3):
-        gemm(a, b, M, N, K, a_mn, b_mn, c=c)
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        gemm(a, b, M, N, K, a_mn, b_mn, c=c)
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    tf = 2 * M * N * K / ms / 1e9
-    # torch reference timing
-    at = a.t() if a_mn else a
-    bt = b if b_mn else b.t()
-    for _ in range(3):
-        torch.mm(at, bt)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(iters):
-        torch.mm(at, bt)
-    e1.record()
-    torch.cuda.synchronize()
-    ms_t = e0.elapsed_time(e1) / iters
-    print(f"BENCH M={M} N={N} K={K} a_mn={a_mn} b_mn={b_mn}: gvl {ms*1e3:.1f}us {tf:.0f} TF/s | "
-          f"torch {ms_t*1e3:.1f}us {2*M*N*K/ms_t/1e9:.0f} TF/s", flush=True)
+    return e0.elapsed_time(e1) / iters
+
+
+def bench(M, N, Kd, am, bm):
+    a, b, A, B = mk(M, N, Kd, am, bm)
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    fl = 2.0 * M * N * Kd
+    row = [f"M={M} N={N} K={Kd} a_mn={am} b_mn={bm}:"]
+    for name, impl, cfg in IMPLS:
+        L.gvl_gemm_tune(impl, cfg)
+        ms = timeit(lambda: K.gemm(A, B, a_mn=bool(am), b_mn=bool(bm), out=c))
+        row.append(f"{name} {fl / ms / 1e9:.0f}")
+    L.gvl_gemm_tune(1, -1)
+    at = A.t() if am else A
+    bt = B if bm else B.t()
+    ms = timeit(lambda: torch.mm(at, bt))
+    row.append(f"torch {fl / ms / 1e9:.0f} TF/s")
+    print(" | ".join(row), flush=True)
 
 
 if __name__ == "__main__":
-    worst = 0
-    for (am, bm) in [(0, 0), (0, 1), (1, 0), (1, 1)]:
-        worst = max(worst, check(256, 256, 128, am, bm))
-        worst = max(worst, check(200, 136, 72, am, bm))
-    worst = max(worst, check(384, 512, 768, 0, 0, bias=True, act=1))
-    worst = max(worst, check(384, 512, 768, 0, 0, bias=True, act=2, res=True))
-    print("WORST", worst, flush=True)
+    w = check()
     for shp in [(8064, 768, 768, 0, 0), (8064, 2304, 768, 0, 0), (8064, 3072, 768, 0, 0),
                 (8064, 768, 3072, 0, 0), (8064, 50304, 768, 0, 0), (8064, 768, 2304, 0, 1),
-                (8064, 768, 3072, 0, 1), (3968, 768, 50304, 0, 1), (16384, 2304, 768, 0, 0),
-                (768, 3072, 16384, 1, 1), (50304, 768, 16384, 1, 1), (8192, 8192, 8192, 0, 0)]:
+                (8064, 768, 3072, 0, 1), (8064, 3072, 768, 0, 1), (3968, 768, 50304, 0, 1),
+                (16384, 2304, 768, 0, 0), (16384, 50304, 768, 0, 0), (16384, 768, 3072, 0, 1),
+                (768, 3072, 16384, 1, 1), (50304, 768, 16384, 1, 1), (4096, 3072, 768, 0, 0),
+                (8192, 8192, 8192, 0, 0)]:
         bench(*shp)
+    sys.exit(0 if w < 1e-2 else 1)
