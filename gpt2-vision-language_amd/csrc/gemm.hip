@@ -172,6 +172,20 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
   return 0;
 }
 
+extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
+  GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
+  const char* tf[2] = {"false", "true"};
+  if (env().impl == 1 && gvl::gemm_lds_ok(d)) {
+    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg);
+    const int bm[3] = {256, 256, 128}, bn[3] = {256, 128, 128}, wm[3] = {2, 4, 2}, wn[3] = {4, 2, 2};
+    snprintf(buf, len, "gemm_lds_kernel<%d, %d, %d, %d, %s, %s>", bm[cfg], bn[cfg], wm[cfg],
+             wn[cfg], tf[d->a_mn != 0], tf[d->b_mn != 0]);
+  } else {
+    snprintf(buf, len, "gemm_bf16_kernel<%s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0]);
+  }
+  return 0;
+}
+
 extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GVL_REQUIRE(d != nullptr, "gvl_gemm: null descriptor");
   GVL_REQUIRE(d->m >= 0 && d->n >= 0 && d->k >= 0, "gvl_gemm: negative size");

@@ -66,6 +66,7 @@ SIGNATURES = {
     "gvl_abi_version": (C.c_int, []),
     "gvl_gemm": (C.c_int, [C.POINTER(GemmDesc), c_vp]),
     "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
+    "gvl_gemm_kernel_name": (C.c_int, [C.POINTER(GemmDesc), C.c_char_p, c_i32]),
     "gvl_layernorm_fwd": (C.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                     c_i64, c_i64, c_f32, c_vp]),
     "gvl_layernorm_bwd_workspace_size": (c_i64, [c_i64, c_i64]),

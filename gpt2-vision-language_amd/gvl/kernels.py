@@ -135,7 +135,9 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
         e0.record()
         _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
         e1.record()
-        _timer.records.append((GEMM_NAMES[(int(a_mn), int(b_mn))], e0, e1, 2.0 * M * N * K))
+        buf = C.create_string_buffer(128)
+        _L().gvl_gemm_kernel_name(C.byref(d), buf, 128)
+        _timer.records.append((buf.value.decode(), e0, e1, 2.0 * M * N * K))
         return out
     _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
     return out

@@ -73,6 +73,9 @@ int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
  * kernel when K % 64 == 0 (default), 0 = register-staged kernel always; cfg -1 = pick
  * the tile by shape, 0/1/2 = force 256x256 / 256x128 / 128x128. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
+/* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
+ * caller attribute event timings to the rocprofv3 kernel-trace rows). */
+int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (eps given; reference uses 1e-5).
