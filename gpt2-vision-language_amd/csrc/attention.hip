@@ -1,18 +1,19 @@
 // Fused attention for head dim 64 on gfx950 MFMA (16x16x32 bf16), forward + backward.
 //
-// Forward (flash-style, online softmax in fp32): block = (64-query tile, head, batch),
-// 4 waves x 16 query rows.  K and V tiles of 64 keys are register-staged into a
-// double-buffered LDS ring.  S is computed "swapped" (K fragment as the MFMA A operand),
+// Forward (flash-style, online softmax in fp32): block = (64*G-query tile, head, batch),
+// 4 waves x G groups of 16 query rows.  K and V tiles of 64 keys are register-staged into
+// a double-buffered LDS ring.  S is computed "swapped" (K fragment as the MFMA A operand),
 // which leaves one query row per lane (lane&15) and 16 keys in registers, so the row
 // max/sum need only two cross-lane steps, and the P fragment of the following P.V MFMA is
 // lane-local (the MFMA k-slots are permuted to match; V is read with ds_read_b64_tr_b16).
 // The output accumulator keeps the same query on the lane, so rescales are lane-local.
+// With G = 2 every K/V fragment read from LDS feeds two MFMAs (two query groups).
 //
 // Backward (FA2 recompute, no atomics, deterministic): a preprocess kernel computes
 // D = rowsum(dO*O); dQ is produced by a query-tile kernel looping over key tiles and
-// dK/dV by a key-tile kernel looping over query tiles.  P is recomputed from the saved
-// log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash mask on (b,h,q,k), identical in
-// every kernel.
+// dK/dV by a key-tile kernel (G groups of 16 keys per wave) looping over query tiles.
+// P is recomputed from the saved log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash
+// mask on (b,h,q,k), identical in every kernel.
 #include "common.h"
 #include "capi_util.h"
 #include "../../include/gvl.h"
@@ -20,8 +21,7 @@
 namespace {
 
 constexpr int D = 64;        // head dim
-constexpr int QT = 64;       // query tile per block
-constexpr int KT = 64;       // key tile
+constexpr int KT = 64;       // key tile (forward / dq) and query tile (dkdv)
 constexpr int NT = 256;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
@@ -104,21 +104,28 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 }
 
 // ------------------------------------------------------------------------------------
+template <int G>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
+  constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int G = lane >> 4;
+  const int Gl = lane >> 4;
   const int64_t b = blockIdx.z, h = blockIdx.y;
   const int64_t qblk0 = (int64_t)blockIdx.x * QT;
-  const int64_t q = qblk0 + wave * 16 + (lane & 15);
-  const bool qok = q < p.Tq;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
 
-  short8_t qf[2];
-  qf[0] = load_frag_global(qbase + q * p.q_st, 0, lane, qok);
-  qf[1] = load_frag_global(qbase + q * p.q_st, 1, lane, qok);
+  int64_t q[G];
+  bool qok[G];
+  short8_t qf[G][2];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    qok[g] = q[g] < p.Tq;
+    qf[g][0] = load_frag_global(qbase + q[g] * p.q_st, 0, lane, qok[g]);
+    qf[g][1] = load_frag_global(qbase + q[g] * p.q_st, 1, lane, qok[g]);
+  }
 
   int64_t kend = p.Tk;
   if (p.causal) {
@@ -127,11 +134,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
   }
   const int nkt = (int)((kend + KT - 1) / KT);
 
-  float4_t o[4];
+  float4_t o[G][4];
+  float m[G], l[G];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) o[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
-  const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q) * (uint64_t)p.Tk;
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+  }
 
   uint4 rk[2], rv[2];
   load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
@@ -149,53 +160,68 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
     const char* ks = smem[kt & 1][0];
     const char* vs = smem[kt & 1][1];
     const int64_t k0 = (int64_t)kt * KT;
-    float4_t sc[4];
+    float4_t sc[G][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) sc[n] = mfma16(frag_row(ks, 16 * n, s, lane), qf[s], sc[n]);
+      for (int g = 0; g < G; ++g) sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const short8_t kf = frag_row(ks, 16 * n, s, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) sc[g][n] = mfma16(kf, qf[g][s], sc[g][n]);
+      }
     }
-    // scale + mask; lane holds S[q][key = k0 + 16n + 4G + r]
-    float mx = -INFINITY;
+    short8_t pf[G][2];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int g = 0; g < G; ++g) {
+      // scale + mask; lane holds S[q][key = k0 + 16n + 4Gl + r]
+      float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t key = k0 + 16 * n + 4 * G + r;
-        float sv = sc[n][r] * p.c2;
-        if (key >= p.Tk || (p.causal && key > q)) sv = -INFINITY;
-        sc[n][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float msub = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(m - msub);
-    m = mnew;
-    float ls = 0.f;
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(sc[n][r] - msub);
-        ls += e;
-        float pe = e;
-        if (p.has_drop) {
-          const int64_t key = k0 + 16 * n + 4 * G + r;
-          pe = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const int64_t key = k0 + 16 * n + 4 * Gl + r;
+          float sv = sc[g][n][r] * p.c2;
+          if (key >= p.Tk || (p.causal && key > q[g])) sv = -INFINITY;
+          sc[g][n][r] = sv;
+          mx = fmaxf(mx, sv);
         }
-        sc[n][r] = pe;
-      }
-    l = l * alpha + ls;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m[g], mx);
+      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = exp2f(m[g] - msub);
+      m[g] = mnew;
+      float ls = 0.f;
+      const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q[g]) * (uint64_t)p.Tk;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] *= alpha;
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(sc[g][n][r] - msub);
+          ls += e;
+          float pe = e;
+          if (p.has_drop) {
+            const int64_t key = k0 + 16 * n + 4 * Gl + r;
+            pe = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
+          }
+          sc[g][n][r] = pe;
+        }
+      l[g] = l[g] * alpha + ls;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[g][t] *= alpha;
+      pf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+      pf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const short8_t pf = pack_frag(sc[2 * s], sc[2 * s + 1]);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = mfma16(frag_tr<true>(vs, t, s, lane), pf, o[t]);
+      for (int t = 0; t < 4; ++t) {
+        const short8_t vf = frag_tr<true>(vs, t, s, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) o[g][t] = mfma16(vf, pf[g][s], o[g][t]);
+      }
     }
     if (more) {
       store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
@@ -203,18 +229,22 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
     }
     __syncthreads();
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (!qok) return;
-  const float inv = 1.f / l;
-  bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q * p.o_st;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int d = 16 * t + 4 * G;
-    *reinterpret_cast<uint2*>(orow + d) =
-        make_uint2(pack2(o[t][0] * inv, o[t][1] * inv), pack2(o[t][2] * inv, o[t][3] * inv));
+  for (int g = 0; g < G; ++g) {
+    float lt = l[g];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (!qok[g]) continue;
+    const float inv = 1.f / lt;
+    bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q[g] * p.o_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(orow + d) = make_uint2(pack2(o[g][t][0] * inv, o[g][t][1] * inv),
+                                                       pack2(o[g][t][2] * inv, o[g][t][3] * inv));
+    }
+    if (Gl == 0 && p.lse) p.lse[(b * p.H + h) * p.Tq + q[g]] = (m[g] + log2f(lt)) * LN2;
   }
-  if (G == 0 && p.lse) p.lse[(b * p.H + h) * p.Tq + q] = (m + log2f(l)) * LN2;
 }
 
 // ------------------------------------------------------------------------------------
@@ -238,29 +268,38 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
   g.Dws[idx] = s;
 }
 
-// dQ: block = (64-query tile, head, batch), waves own 16 query rows each.
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG g) {
+// dQ: block = (64*G-query tile, head, batch), each wave G groups of 16 query rows.
+template <int G>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
+  constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int G = lane >> 4;
+  const int Gl = lane >> 4;
   const int64_t b = blockIdx.z, h = blockIdx.y;
   const int64_t qblk0 = (int64_t)blockIdx.x * QT;
-  const int64_t q = qblk0 + wave * 16 + (lane & 15);
-  const bool qok = q < p.Tq;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
-  const bf16_t* dobase = g.dout + b * g.do_sb + h * g.do_sh;
+  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
-  short8_t qf[2], df[2];
+  int64_t q[G];
+  bool qok[G];
+  short8_t qf[G][2], df[G][2];
+  float lse2[G], Dq[G];
+  uint64_t drow[G];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    qf[s] = load_frag_global(qbase + q * p.q_st, s, lane, qok);
-    df[s] = load_frag_global(dobase + q * g.do_st, s, lane, qok);
+  for (int g = 0; g < G; ++g) {
+    q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    qok[g] = q[g] < p.Tq;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qf[g][s] = load_frag_global(qbase + q[g] * p.q_st, s, lane, qok[g]);
+      df[g][s] = load_frag_global(dobase + q[g] * gg.do_st, s, lane, qok[g]);
+    }
+    const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
+    lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
+    Dq[g] = qok[g] ? gg.Dws[ridx] : 0.f;
+    drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
   }
-  const int64_t ridx = (b * p.H + h) * p.Tq + q;
-  const float lse2 = qok ? p.lse[ridx] * LOG2E : 0.f;
-  const float Dq = qok ? g.Dws[ridx] : 0.f;
-  const uint64_t drow = (uint64_t)ridx * (uint64_t)p.Tk;
 
   int64_t kend = p.Tk;
   if (p.causal) {
@@ -268,9 +307,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG g) {
     if (lim < kend) kend = lim;
   }
   const int nkt = (int)((kend + KT - 1) / KT);
-  float4_t acc[4];
+  float4_t acc[G][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   uint4 rk[2], rv[2];
   load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
@@ -287,34 +328,51 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG g) {
     const char* ks = smem[kt & 1][0];
     const char* vs = smem[kt & 1][1];
     const int64_t k0 = (int64_t)kt * KT;
-    float4_t sc[4], dp[4];
+    float4_t sc[G][4], dp[G][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
-      dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+        dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        sc[n] = mfma16(frag_row(ks, 16 * n, s, lane), qf[s], sc[n]);
-        dp[n] = mfma16(frag_row(vs, 16 * n, s, lane), df[s], dp[n]);
+        const short8_t kf = frag_row(ks, 16 * n, s, lane);
+        const short8_t vf = frag_row(vs, 16 * n, s, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          sc[g][n] = mfma16(kf, qf[g][s], sc[g][n]);
+          dp[g][n] = mfma16(vf, df[g][s], dp[g][n]);
+        }
       }
     }
+    short8_t sf[G][2];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t key = k0 + 16 * n + 4 * G + r;
-        const bool ok = qok && key < p.Tk && !(p.causal && key > q);
-        const float pv = ok ? exp2f(sc[n][r] * p.c2 - lse2) : 0.f;
-        float dpv = dp[n][r];
-        if (p.has_drop)
-          dpv = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? dpv * p.drop_scale : 0.f;
-        sc[n][r] = pv * (dpv - Dq);  // dS
-      }
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t key = k0 + 16 * n + 4 * Gl + r;
+          const bool ok = qok[g] && key < p.Tk && !(p.causal && key > q[g]);
+          const float pv = ok ? exp2f(sc[g][n][r] * p.c2 - lse2[g]) : 0.f;
+          float dpv = dp[g][n][r];
+          if (p.has_drop)
+            dpv = rng_keep(p.seed, drow[g] + (uint64_t)key, p.drop_thresh) ? dpv * p.drop_scale : 0.f;
+          sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
+        }
+      sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+      sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const short8_t sf = pack_frag(sc[2 * s], sc[2 * s + 1]);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = mfma16(frag_tr<false>(ks, t, s, lane), sf, acc[t]);
+      for (int t = 0; t < 4; ++t) {
+        const short8_t kf = frag_tr<false>(ks, t, s, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g][t] = mfma16(kf, sf[g][s], acc[g][t]);
+      }
     }
     if (more) {
       store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
@@ -322,63 +380,76 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG g) {
     }
     __syncthreads();
   }
-  if (!qok) return;
-  bf16_t* dst = g.dq + b * g.dq_sb + h * g.dq_sh + q * g.dq_st;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int d = 16 * t + 4 * G;
-    *reinterpret_cast<uint2*>(dst + d) =
-        make_uint2(pack2(acc[t][0] * p.scale, acc[t][1] * p.scale),
-                   pack2(acc[t][2] * p.scale, acc[t][3] * p.scale));
+  for (int g = 0; g < G; ++g) {
+    if (!qok[g]) continue;
+    bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + q[g] * gg.dq_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(dst + d) =
+          make_uint2(pack2(acc[g][t][0] * p.scale, acc[g][t][1] * p.scale),
+                     pack2(acc[g][t][2] * p.scale, acc[g][t][3] * p.scale));
+    }
   }
 }
 
-// dK/dV: block = (64-key tile, head, batch), waves own 16 keys each; loop over query tiles.
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG g) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][QT * D * 2];  // [stage][Q,dO]
-  __shared__ float sl[2][2][QT];                                       // [stage][lse2, D]
+// dK/dV: block = (64*G-key tile, head, batch), waves own G groups of 16 keys; loop over
+// 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
+template <int G>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
+  constexpr int KB = 64 * G;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
+  __shared__ float sl[2][2][KT];                                       // [stage][lse2, D]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int G = lane >> 4;
+  const int Gl = lane >> 4;
   const int64_t b = blockIdx.z, h = blockIdx.y;
-  const int64_t kblk0 = (int64_t)blockIdx.x * KT;
-  const int64_t key = kblk0 + wave * 16 + (lane & 15);
-  const bool kok = key < p.Tk;
+  const int64_t kblk0 = (int64_t)blockIdx.x * KB;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
-  const bf16_t* dobase = g.dout + b * g.do_sb + h * g.do_sh;
+  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
   const int64_t rbase = (b * p.H + h) * p.Tq;
-  short8_t kf[2], vf[2];
+  int64_t key[G];
+  bool kok[G];
+  short8_t kf[G][2], vf[G][2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    kf[s] = load_frag_global(kbase + key * p.k_st, s, lane, kok);
-    vf[s] = load_frag_global(vbase + key * p.v_st, s, lane, kok);
-  }
-  const int qt_first = p.causal ? (int)(kblk0 / QT) : 0;
-  const int nqt = (int)((p.Tq + QT - 1) / QT);
-  float4_t dk[4], dv[4];
+  for (int g = 0; g < G; ++g) {
+    key[g] = kblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    kok[g] = key[g] < p.Tk;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < 2; ++s) {
+      kf[g][s] = load_frag_global(kbase + key[g] * p.k_st, s, lane, kok[g]);
+      vf[g][s] = load_frag_global(vbase + key[g] * p.v_st, s, lane, kok[g]);
+    }
   }
+  const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
+  const int nqt = (int)((p.Tq + KT - 1) / KT);
+  float4_t dk[G][4], dv[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dk[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+      dv[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    }
   if (qt_first < nqt) {
     uint4 rq[2], rd[2];
     float rl = 0.f, rD = 0.f;
     auto fetch = [&](int qt) {
-      const int64_t q0 = (int64_t)qt * QT;
+      const int64_t q0 = (int64_t)qt * KT;
       load_rows(rq, qbase, p.q_st, q0, p.Tq, tid);
-      load_rows(rd, dobase, g.do_st, q0, p.Tq, tid);
-      if (tid < QT) {
+      load_rows(rd, dobase, gg.do_st, q0, p.Tq, tid);
+      if (tid < KT) {
         const int64_t qq = q0 + tid;
         rl = qq < p.Tq ? p.lse[rbase + qq] * LOG2E : 0.f;
-        rD = qq < p.Tq ? g.Dws[rbase + qq] : 0.f;
+        rD = qq < p.Tq ? gg.Dws[rbase + qq] : 0.f;
       }
     };
     auto put = [&](int st) {
       store_rows<false>(rq, smem[st][0], tid);
       store_rows<false>(rd, smem[st][1], tid);
-      if (tid < QT) {
+      if (tid < KT) {
         sl[st][0][tid] = rl;
         sl[st][1][tid] = rD;
       }
@@ -392,62 +463,85 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG g) 
       if (more) fetch(qt + 1);
       const char* qs = smem[st][0];
       const char* ds = smem[st][1];
-      const int64_t q0 = (int64_t)qt * QT;
-      float4_t sc[4], dp[4];
+      const int64_t q0 = (int64_t)qt * KT;
+      float4_t sc[G][4], dp[G][4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
-        dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+          dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          sc[n] = mfma16(frag_row(qs, 16 * n, s, lane), kf[s], sc[n]);
-          dp[n] = mfma16(frag_row(ds, 16 * n, s, lane), vf[s], dp[n]);
+          const short8_t qfr = frag_row(qs, 16 * n, s, lane);
+          const short8_t dfr = frag_row(ds, 16 * n, s, lane);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            sc[g][n] = mfma16(qfr, kf[g][s], sc[g][n]);
+            dp[g][n] = mfma16(dfr, vf[g][s], dp[g][n]);
+          }
         }
       }
-      // lane holds S[q = q0 + 16n + 4G + r][key]
-      float4_t pd[4];
+      // lane holds S[q = q0 + 16n + 4Gl + r][key[g]]
+      short8_t pf[G][2], sf[G][2];
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+      for (int g = 0; g < G; ++g) {
+        float4_t pd[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qi = 16 * n + 4 * G + r;
-          const int64_t qq = q0 + qi;
-          const bool ok = kok && qq < p.Tq && !(p.causal && key > qq);
-          const float pv = ok ? exp2f(sc[n][r] * p.c2 - sl[st][0][qi]) : 0.f;
-          float pdrop = pv, dpv = dp[n][r];
-          if (p.has_drop) {
-            const bool keep =
-                rng_keep(p.seed, (uint64_t)(rbase + qq) * (uint64_t)p.Tk + (uint64_t)key, p.drop_thresh);
-            pdrop = keep ? pv * p.drop_scale : 0.f;
-            dpv = keep ? dpv * p.drop_scale : 0.f;
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qi = 16 * n + 4 * Gl + r;
+            const int64_t qq = q0 + qi;
+            const bool ok = kok[g] && qq < p.Tq && !(p.causal && key[g] > qq);
+            const float pv = ok ? exp2f(sc[g][n][r] * p.c2 - sl[st][0][qi]) : 0.f;
+            float pdrop = pv, dpv = dp[g][n][r];
+            if (p.has_drop) {
+              const bool keep = rng_keep(
+                  p.seed, (uint64_t)(rbase + qq) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
+              pdrop = keep ? pv * p.drop_scale : 0.f;
+              dpv = keep ? dpv * p.drop_scale : 0.f;
+            }
+            pd[n][r] = pdrop;
+            sc[g][n][r] = pv * (dpv - sl[st][1][qi]);  // dS
           }
-          pd[n][r] = pdrop;
-          sc[n][r] = pv * (dpv - sl[st][1][qi]);  // dS
-        }
+        pf[g][0] = pack_frag(pd[0], pd[1]);
+        pf[g][1] = pack_frag(pd[2], pd[3]);
+        sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+        sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const short8_t pf = pack_frag(pd[2 * s], pd[2 * s + 1]);
-        const short8_t sf = pack_frag(sc[2 * s], sc[2 * s + 1]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          dv[t] = mfma16(frag_tr<false>(ds, t, s, lane), pf, dv[t]);
-          dk[t] = mfma16(frag_tr<false>(qs, t, s, lane), sf, dk[t]);
+          const short8_t dot = frag_tr<false>(ds, t, s, lane);
+          const short8_t qtr = frag_tr<false>(qs, t, s, lane);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            dv[g][t] = mfma16(dot, pf[g][s], dv[g][t]);
+            dk[g][t] = mfma16(qtr, sf[g][s], dk[g][t]);
+          }
         }
       }
       if (more) put(st ^ 1);  // stage st^1 was last read in iteration qt-1
       __syncthreads();
     }
   }
-  if (!kok) return;
-  bf16_t* dkr = g.dk + b * g.dk_sb + h * g.dk_sh + key * g.dk_st;
-  bf16_t* dvr = g.dv + b * g.dv_sb + h * g.dv_sh + key * g.dv_st;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int d = 16 * t + 4 * G;
-    *reinterpret_cast<uint2*>(dkr + d) =
-        make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale), pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
-    *reinterpret_cast<uint2*>(dvr + d) =
-        make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+  for (int g = 0; g < G; ++g) {
+    if (!kok[g]) continue;
+    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + key[g] * gg.dk_st;
+    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + key[g] * gg.dv_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(dkr + d) =
+          make_uint2(pack2(dk[g][t][0] * p.scale, dk[g][t][1] * p.scale),
+                     pack2(dk[g][t][2] * p.scale, dk[g][t][3] * p.scale));
+      *reinterpret_cast<uint2*>(dvr + d) =
+          make_uint2(pack2(dv[g][t][0], dv[g][t][1]), pack2(dv[g][t][2], dv[g][t][3]));
+    }
   }
 }
 
@@ -482,13 +576,19 @@ int fill(const gvl_attn_desc* d, AttnP& p) {
   return 0;
 }
 
+// Two query groups per wave (128-row blocks) only pay off once a block has enough rows;
+// the short caption sequences (31-64 rows) keep 64-row blocks.
+int pick_groups(int64_t T) { return T > 64 ? 2 : 1; }
+
 }  // namespace
 
 extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   AttnP p;
   if (fill(d, p)) return -1;
-  dim3 grid((unsigned)((d->Tq + QT - 1) / QT), (unsigned)d->H, (unsigned)d->B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(NT), 0, gvl::as_stream(stream), p);
+  const int G = pick_groups(d->Tq);
+  dim3 grid((unsigned)((d->Tq + 64 * G - 1) / (64 * G)), (unsigned)d->H, (unsigned)d->B);
+  if (G == 2) hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(NT), 0, gvl::as_stream(stream), p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(NT), 0, gvl::as_stream(stream), p);
   GVL_LAUNCH_CHECK("gvl_attn_fwd");
   return 0;
 }
@@ -520,11 +620,15 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   const int64_t rows = d->B * d->H * d->Tq;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
-  dim3 gq((unsigned)((d->Tq + QT - 1) / QT), (unsigned)d->H, (unsigned)d->B);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(NT), 0, s, p, g);
+  const int Gq = pick_groups(d->Tq);
+  dim3 gq((unsigned)((d->Tq + 64 * Gq - 1) / (64 * Gq)), (unsigned)d->H, (unsigned)d->B);
+  if (Gq == 2) hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, gq, dim3(NT), 0, s, p, g);
+  else hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, gq, dim3(NT), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
-  dim3 gk((unsigned)((d->Tk + KT - 1) / KT), (unsigned)d->H, (unsigned)d->B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, gk, dim3(NT), 0, s, p, g);
+  // dK/dV keeps one 16-key group per wave: two groups need >256 VGPRs (dK and dV
+  // accumulators for 32 keys x 64 dims) and spill to scratch.
+  dim3 gk((unsigned)((d->Tk + 63) / 64), (unsigned)d->H, (unsigned)d->B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, gk, dim3(NT), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");
   return 0;
 }

@@ -148,12 +148,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
   gemm_epilogue<4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-// GVL_GEMM_IMPL=regstage forces the fallback; GVL_GEMM_CFG=0|1|2 forces a tile config.
+// GVL_GEMM_IMPL=regstage|lds|ring picks the kernel family (0|1|2); GVL_GEMM_CFG=0..3 forces
+// a tile config of that family.
 struct GemmEnv {
   int impl = 1, cfg = -1;
   GemmEnv() {
     const char* s = getenv("GVL_GEMM_IMPL");
-    if (s && s[0] == 'r') impl = 0;
+    if (s && s[0] == 'r' && s[1] == 'e') impl = 0;
+    if (s && s[0] == 'l') impl = 1;
+    if (s && s[0] == 'r' && s[1] == 'i') impl = 2;
     const char* c = getenv("GVL_GEMM_CFG");
     if (c) cfg = atoi(c);
   }
@@ -166,7 +169,7 @@ GemmEnv& env() {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 1 && cfg >= -1 && cfg <= 2, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 2 && cfg >= -1 && cfg <= 5, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -175,8 +178,11 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
-  if (env().impl == 1 && gvl::gemm_lds_ok(d)) {
-    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg);
+  if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
+    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
+    snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(cfg), tf[d->a_mn != 0], tf[d->b_mn != 0]);
+  } else if (env().impl >= 1 && gvl::gemm_lds_ok(d)) {
+    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg > 2 ? -1 : env().cfg);
     const int bm[3] = {256, 256, 128}, bn[3] = {256, 128, 128}, wm[3] = {2, 4, 2}, wn[3] = {4, 2, 2};
     snprintf(buf, len, "gemm_lds_kernel<%d, %d, %d, %d, %s, %s>", bm[cfg], bn[cfg], wm[cfg],
              wn[cfg], tf[d->a_mn != 0], tf[d->b_mn != 0]);
@@ -231,8 +237,14 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
              ? static_cast<float*>(d->workspace) : nullptr;
   p.ws_bytes = p.ws ? d->workspace_bytes : 0;
   hipStream_t s = gvl::as_stream(stream);
-  if (env().impl == 1 && gvl::gemm_lds_ok(d)) {
-    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg);
+  if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
+    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
+    gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, cfg, s);
+    GVL_LAUNCH_CHECK("gvl_gemm(ring)");
+    return 0;
+  }
+  if (env().impl >= 1 && gvl::gemm_lds_ok(d)) {
+    const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg > 2 ? -1 : env().cfg);
     gvl::gemm_lds_launch(p, d->a_mn, d->b_mn, cfg, s);
     GVL_LAUNCH_CHECK("gvl_gemm(lds)");
     return 0;

@@ -143,4 +143,9 @@ int gemm_lds_pick(int64_t M, int64_t N, int64_t K, int forced);
 int gemm_splitk_pick(int64_t tiles, int64_t K);
 bool gemm_lds_ok(const gvl_gemm_desc* d);
 int gemm_lds_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
+void gemm_splitk_reduce_launch(const GemmP& p, hipStream_t s);
+const char* gemm_ring_name(int cfg);
+bool gemm_ring_ok(const gvl_gemm_desc* d);
+int gemm_ring_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
+int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced);
 }  // namespace gvl

@@ -192,10 +192,7 @@ int launch_cfg(const GemmP& p0, hipStream_t s) {
   p.kper = p.splits > 1 ? ((p.K / p.splits + BK - 1) / BK) * BK : p.K;
   if (p.splits > 1) p.splits = (int)((p.K + p.kper - 1) / p.kper);
   hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(64 * WMW * WNW), lds, s, p);
-  if (p.splits > 1) {
-    const int64_t quads = p.M * (p.N >> 2);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, p);
-  }
+  if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }
 
@@ -211,6 +208,11 @@ int launch_layout(const GemmP& p, int cfg, hipStream_t s) {
 }  // namespace
 
 namespace gvl {
+void gemm_splitk_reduce_launch(const GemmP& p, hipStream_t s) {
+  const int64_t quads = p.M * (p.N >> 2);
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, p);
+}
+
 // Tile choice: estimated time = waves-of-tiles x tile work / relative per-CU efficiency.
 // Measured on MI355X (tools/gpu_probe_gemm.py, profiles/r1): 128x128 (2 WGs/CU) wins for the
 // caption-step shapes (M ~ 8k, N 768-3072); 256x256 only once there are >= 2 tiles per CU.

@@ -11,7 +11,10 @@ from gvl import kernels as K  # noqa: E402
 
 L = _lib.load()
 IMPLS = [("regstage", 0, -1), ("lds256x256", 1, 0), ("lds256x128", 1, 1), ("lds128x128", 1, 2),
-         ("lds-auto", 1, -1)]
+         ("lds-auto", 1, -1), ("ring256", 2, 0), ("ring256x128", 2, 1), ("ring128", 2, 2),
+         ("ring256s5", 2, 3), ("pp4", 2, 4), ("pp5", 2, 5)]
+if os.environ.get("PROBE_ONLY_RING"):
+    IMPLS = [x for x in IMPLS if x[1] == 2 or x[0] == "lds-auto"]
 
 
 def mk(M, N, Kd, a_mn, b_mn, seed=0):
@@ -27,7 +30,8 @@ def check():
     worst = 0.0
     for name, impl, cfg in IMPLS:
         L.gvl_gemm_tune(impl, cfg)
-        for (M, N, Kd) in [(256, 256, 128), (200, 136, 192), (520, 264, 256), (64, 8, 64)]:
+        for (M, N, Kd) in [(256, 256, 128), (200, 136, 192), (520, 264, 256), (64, 8, 64),
+                           (264, 520, 96), (1032, 1024, 1024)]:
             for am, bm in [(0, 0), (0, 1), (1, 0), (1, 1)]:
                 if (am and M % 8) or (bm and N % 8):
                     continue
