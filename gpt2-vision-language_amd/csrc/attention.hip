@@ -175,21 +175,27 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
     short8_t pf[G][2];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      // scale + mask; lane holds S[q][key = k0 + 16n + 4Gl + r]
+      // lane holds raw S[q][key = k0 + 16n + 4Gl + r]; masks only on boundary / diagonal
+      // tiles (wave-uniform test), the softmax scale folded into the exp2 argument
+      const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
+      if (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0)) {
+        const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kk = 16 * n + 4 * Gl + r;
+            if (kk >= kl || (p.causal && kk > ql)) sc[g][n][r] = -INFINITY;
+          }
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t key = k0 + 16 * n + 4 * Gl + r;
-          float sv = sc[g][n][r] * p.c2;
-          if (key >= p.Tk || (p.causal && key > q[g])) sv = -INFINITY;
-          sc[g][n][r] = sv;
-          mx = fmaxf(mx, sv);
-        }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[g][n][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[g], mx);
+      const float mnew = fmaxf(m[g], mx * p.c2);
       const float msub = (mnew == -INFINITY) ? 0.f : mnew;
       const float alpha = exp2f(m[g] - msub);
       m[g] = mnew;
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(sc[g][n][r] - msub);
+          const float e = exp2f(fmaf(sc[g][n][r], p.c2, -msub));
           ls += e;
           float pe = e;
           if (p.has_drop) {
@@ -350,16 +356,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
     short8_t sf[G][2];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      // rows past Tq and keys past Tk meet zero Q/dO/K/V rows, so only the causal diagonal
+      // and the ragged last key tile need the explicit mask (wave-uniform test)
+      const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
+      const bool msk = k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0);
+      const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t key = k0 + 16 * n + 4 * Gl + r;
-          const bool ok = qok[g] && key < p.Tk && !(p.causal && key > q[g]);
-          const float pv = ok ? exp2f(sc[g][n][r] * p.c2 - lse2[g]) : 0.f;
+          const int kk = 16 * n + 4 * Gl + r;
+          float pv = exp2f(fmaf(sc[g][n][r], p.c2, -lse2[g]));
+          if (msk && (kk >= kl || (p.causal && kk > ql))) pv = 0.f;
           float dpv = dp[g][n][r];
           if (p.has_drop)
-            dpv = rng_keep(p.seed, drow[g] + (uint64_t)key, p.drop_thresh) ? dpv * p.drop_scale : 0.f;
+            dpv = rng_keep(p.seed, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
           sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
         }
       sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
@@ -400,7 +411,7 @@ template <int G>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
   constexpr int KB = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
-  __shared__ float sl[2][2][KT];                                       // [stage][lse2, D]
+  __shared__ __attribute__((aligned(16))) float sl[2][2][KT];         // [stage][lse2, D]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   const int64_t b = blockIdx.z, h = blockIdx.y;
@@ -483,28 +494,39 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg)
           }
         }
       }
-      // lane holds S[q = q0 + 16n + 4Gl + r][key[g]]
+      // lane holds S[q = q0 + 16n + 4Gl + r][key[g]]; lse and D of those 4 consecutive
+      // queries come from LDS as one float4 each
       short8_t pf[G][2], sf[G][2];
+      float4 l4[4], d4[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        l4[n] = *reinterpret_cast<const float4*>(&sl[st][0][16 * n + 4 * Gl]);
+        d4[n] = *reinterpret_cast<const float4*>(&sl[st][1][16 * n + 4 * Gl]);
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
+        const int64_t kg_max = kblk0 + wave * 16 * G + g * 16 + 15;
+        const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
+        const int qlim = (int)(p.Tq - q0), kq = (int)(key[g] - q0);
         float4_t pd[4];
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qi = 16 * n + 4 * Gl + r;
-            const int64_t qq = q0 + qi;
-            const bool ok = kok[g] && qq < p.Tq && !(p.causal && key[g] > qq);
-            const float pv = ok ? exp2f(sc[g][n][r] * p.c2 - sl[st][0][qi]) : 0.f;
+            const float lr = r == 0 ? l4[n].x : r == 1 ? l4[n].y : r == 2 ? l4[n].z : l4[n].w;
+            const float dr = r == 0 ? d4[n].x : r == 1 ? d4[n].y : r == 2 ? d4[n].z : d4[n].w;
+            float pv = exp2f(fmaf(sc[g][n][r], p.c2, -lr));
+            if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
             float pdrop = pv, dpv = dp[g][n][r];
             if (p.has_drop) {
               const bool keep = rng_keep(
-                  p.seed, (uint64_t)(rbase + qq) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
+                  p.seed, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
               pdrop = keep ? pv * p.drop_scale : 0.f;
               dpv = keep ? dpv * p.drop_scale : 0.f;
             }
             pd[n][r] = pdrop;
-            sc[g][n][r] = pv * (dpv - sl[st][1][qi]);  // dS
+            sc[g][n][r] = pv * (dpv - dr);  // dS
           }
         pf[g][0] = pack_frag(pd[0], pd[1]);
         pf[g][1] = pack_frag(pd[2], pd[3]);

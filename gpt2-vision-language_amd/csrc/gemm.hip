@@ -151,8 +151,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
 // GVL_GEMM_IMPL=regstage|lds|ring picks the kernel family (0|1|2); GVL_GEMM_CFG=0..3 forces
 // a tile config of that family.
 struct GemmEnv {
-  int impl = 1, cfg = -1;
+  int impl = 2, cfg = -1, group = 8;
   GemmEnv() {
+    const char* gr = getenv("GVL_GEMM_GROUP");
+    if (gr && atoi(gr) > 0) group = atoi(gr);
     const char* s = getenv("GVL_GEMM_IMPL");
     if (s && s[0] == 'r' && s[1] == 'e') impl = 0;
     if (s && s[0] == 'l') impl = 1;
@@ -233,6 +235,7 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
   p.splits = 1;
   p.kper = d->k;
+  p.group = env().group;
   p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
              ? static_cast<float*>(d->workspace) : nullptr;
   p.ws_bytes = p.ws ? d->workspace_bytes : 0;

@@ -21,6 +21,7 @@ struct GemmP {
   float drop_scale;
   uint32_t drop_thresh;
   int tiles_m, tiles_n;
+  int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
   // writing fp32 partials to ws[s][M][N]; gemm_splitk_reduce applies the epilogue.
@@ -29,6 +30,26 @@ struct GemmP {
   float* ws;
   int64_t ws_bytes;
 };
+
+// Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
+// XCD (blockIdx % 8) owns a contiguous range of work items, then that range is walked in
+// groups of `group` tile rows, column by column: the ~32-64 tiles an XCD runs at once form a
+// group x (32-64 / group) block and share A and B panels in that XCD's L2 (a row-major walk
+// shares only the A panel and streams every B panel from HBM/MALL).
+GVL_DEV void gemm_work_tile(int splits, int tiles_m, int tiles_n, int group, int& split, int& tm,
+                            int& tn) {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  split = work % splits;
+  const int tile = work / splits;
+  const int per_group = group * tiles_n;
+  const int grp = tile / per_group, first_m = grp * group;
+  const int gsz = tiles_m - first_m < group ? tiles_m - first_m : group;
+  const int in = tile - grp * per_group;
+  tm = first_m + in % gsz;
+  tn = in / gsz;
+}
 
 // Epilogue for accumulators produced with swapped operands: acc[i][j] holds, for this lane,
 // row m = mw0 + 16 i + (lane & 15) and columns n = nw0 + 16 j + 4 (lane >> 4) + r, r = 0..3.

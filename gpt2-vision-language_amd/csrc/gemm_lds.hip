@@ -93,11 +93,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (BM * BN > 16384 ? 1 : 2)) void gem
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
 
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = work % p.splits, tile = work / p.splits;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int split, tm, tn;
+  gemm_work_tile(p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)split * p.kper;
   const int64_t kend = kbeg + p.kper < p.K ? kbeg + p.kper : p.K;

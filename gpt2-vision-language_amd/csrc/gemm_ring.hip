@@ -116,12 +116,8 @@ __global__ __launch_bounds__(64 * WMW * WNW, (BM * BN > 16384 ? 1 : 2)) void gem
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
 
-  // XCD-aware bijective remap (consecutive work items share an XCD's L2)
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = work % p.splits, tile = work / p.splits;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int split, tm, tn;
+  gemm_work_tile(p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)split * p.kper;
   const int64_t kend = kbeg + p.kper < p.K ? kbeg + p.kper : p.K;
@@ -266,11 +262,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = wave >> 2, wc = wave & 3;
 
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = work % p.splits, tile = work / p.splits;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int split, tm, tn;
+  gemm_work_tile(p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = (int64_t)split * p.kper;
   const int64_t kend = kbeg + p.kper < p.K ? kbeg + p.kper : p.K;
@@ -431,11 +424,13 @@ int gemm_ring_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s)
 }  // namespace gvl
 
 namespace gvl {
-// Tile choice for the ring kernels (measured, tools/gpu_probe_gemm.py): the 256x256 tile
-// once the output has about one tile per CU, else 128x128 at two workgroups per CU.
+// Tile choice (measured, tools/gemm_sweep.sh on MI355X): the ping-pong 256x256 kernel once the
+// output has >= 192 of its tiles, except between 1 and 1.25 rounds of 256 CUs (a nearly empty
+// second round); else the 128x128 ring kernel at two workgroups per CU.
 int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced) {
   if (forced >= 0) return forced;
   const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  return t256 >= 240 ? 0 : 2;
+  if (t256 < 192 || (t256 > 256 && t256 <= 320)) return 2;
+  return 4;
 }
 }  // namespace gvl
