@@ -104,7 +104,7 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 }
 
 // ------------------------------------------------------------------------------------
-template <int G>
+template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m[g], mx * p.c2);
       const float msub = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = exp2f(m[g] - msub);
+      const float alpha = __builtin_amdgcn_exp2f(m[g] - msub);
       m[g] = mnew;
       float ls = 0.f;
       const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q[g]) * (uint64_t)p.Tk;
@@ -205,10 +205,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(fmaf(sc[g][n][r], p.c2, -msub));
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -msub));
           ls += e;
           float pe = e;
-          if (p.has_drop) {
+          if constexpr (DROP) {
             const int64_t key = k0 + 16 * n + 4 * Gl + r;
             pe = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
           }
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
 }
 
 // dQ: block = (64*G-query tile, head, batch), each wave G groups of 16 query rows.
-template <int G>
+template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
@@ -366,10 +366,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kk = 16 * n + 4 * Gl + r;
-          float pv = exp2f(fmaf(sc[g][n][r], p.c2, -lse2[g]));
+          float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lse2[g]));
           if (msk && (kk >= kl || (p.causal && kk > ql))) pv = 0.f;
           float dpv = dp[g][n][r];
-          if (p.has_drop)
+          if constexpr (DROP)
             dpv = rng_keep(p.seed, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
           sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
         }
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
 
 // dK/dV: block = (64*G-key tile, head, batch), waves own G groups of 16 keys; loop over
 // 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
-template <int G>
+template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
   constexpr int KB = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
@@ -516,10 +516,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg)
             const int qi = 16 * n + 4 * Gl + r;
             const float lr = r == 0 ? l4[n].x : r == 1 ? l4[n].y : r == 2 ? l4[n].z : l4[n].w;
             const float dr = r == 0 ? d4[n].x : r == 1 ? d4[n].y : r == 2 ? d4[n].z : d4[n].w;
-            float pv = exp2f(fmaf(sc[g][n][r], p.c2, -lr));
+            float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lr));
             if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
             float pdrop = pv, dpv = dp[g][n][r];
-            if (p.has_drop) {
+            if constexpr (DROP) {
               const bool keep = rng_keep(
                   p.seed, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
               pdrop = keep ? pv * p.drop_scale : 0.f;
@@ -609,8 +609,14 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   if (fill(d, p)) return -1;
   const int G = pick_groups(d->Tq);
   dim3 grid((unsigned)((d->Tq + 64 * G - 1) / (64 * G)), (unsigned)d->H, (unsigned)d->B);
-  if (G == 2) hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(NT), 0, gvl::as_stream(stream), p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(NT), 0, gvl::as_stream(stream), p);
+  hipStream_t s = gvl::as_stream(stream);
+  if (G == 2) {
+    if (p.has_drop) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<2, false>), grid, dim3(NT), 0, s, p);
+  } else {
+    if (p.has_drop) hipLaunchKernelGGL((attn_fwd_kernel<1, true>), grid, dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<1, false>), grid, dim3(NT), 0, s, p);
+  }
   GVL_LAUNCH_CHECK("gvl_attn_fwd");
   return 0;
 }
@@ -644,13 +650,19 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
   const int Gq = pick_groups(d->Tq);
   dim3 gq((unsigned)((d->Tq + 64 * Gq - 1) / (64 * Gq)), (unsigned)d->H, (unsigned)d->B);
-  if (Gq == 2) hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, gq, dim3(NT), 0, s, p, g);
-  else hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, gq, dim3(NT), 0, s, p, g);
+  if (Gq == 2) {
+    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), gq, dim3(NT), 0, s, p, g);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), gq, dim3(NT), 0, s, p, g);
+  } else {
+    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<1, true>), gq, dim3(NT), 0, s, p, g);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<1, false>), gq, dim3(NT), 0, s, p, g);
+  }
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
   // dK/dV keeps one 16-key group per wave: two groups need >256 VGPRs (dK and dV
   // accumulators for 32 keys x 64 dims) and spill to scratch.
   dim3 gk((unsigned)((d->Tk + 63) / 64), (unsigned)d->H, (unsigned)d->B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, gk, dim3(NT), 0, s, p, g);
+  if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), gk, dim3(NT), 0, s, p, g);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), gk, dim3(NT), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");
   return 0;
 }

@@ -36,11 +36,13 @@ struct GemmP {
 // groups of `group` tile rows, column by column: the ~32-64 tiles an XCD runs at once form a
 // group x (32-64 / group) block and share A and B panels in that XCD's L2 (a row-major walk
 // shares only the A panel and streams every B panel from HBM/MALL).
-GVL_DEV void gemm_work_tile(int splits, int tiles_m, int tiles_n, int group, int& split, int& tm,
-                            int& tn) {
+GVL_DEV int gemm_xcd_work() {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+GVL_DEV void gemm_tile_of(int work, int splits, int tiles_m, int tiles_n, int group, int& split,
+                          int& tm, int& tn) {
   split = work % splits;
   const int tile = work / splits;
   const int per_group = group * tiles_n;
@@ -49,6 +51,10 @@ GVL_DEV void gemm_work_tile(int splits, int tiles_m, int tiles_n, int group, int
   const int in = tile - grp * per_group;
   tm = first_m + in % gsz;
   tn = in / gsz;
+}
+GVL_DEV void gemm_work_tile(int splits, int tiles_m, int tiles_n, int group, int& split, int& tm,
+                            int& tn) {
+  gemm_tile_of(gemm_xcd_work(), splits, tiles_m, tiles_n, group, split, tm, tn);
 }
 
 // Epilogue for accumulators produced with swapped operands: acc[i][j] holds, for this lane,
