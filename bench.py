@@ -87,10 +87,12 @@ def run_lm(args, world, rank, dev, timer=None):
     batches = [lm_batch(B, T, step=i, rank=rank, device=dev) for i in range(accum)]
     loss_fn = lambda m, b: m(b[0], b[1])[1]
 
-    def step(it):
-        return train_step(model, opt, batches, loss_fn, get_lr(it, 6e-4, 6e-5, 715, 19073),
-                          buckets=buckets)
+    lr_fn = lambda it: get_lr(it, 6e-4, 6e-5, 715, 19073)  # noqa: E731
 
+    def step(it):
+        return train_step(model, opt, batches, loss_fn, lr_fn(it), buckets=buckets)
+
+    step.graph_args = (model, opt, batches, loss_fn, lr_fn)
     tokens_per_step = B * T * accum * world
     return step, tokens_per_step, dict(workload="gpt2-124m-lm-pretrain", micro_batch=B,
                                        seq_len=T, grad_accum=accum,
@@ -115,9 +117,12 @@ def run_caption(kind, args, world, rank, dev):
         lab = caption_labels(y, m)
         loss_fn = lambda mm, b: mm(pool(b[0]), b[1], labels=lab)[1]
 
+    lr_fn = lambda it: get_lr(it, 1e-3, 1e-4, 5, 80)  # noqa: E731
+
     def step(it):
-        return train_step(model, opt, [(z, x, y, m)], loss_fn, get_lr(it, 1e-3, 1e-4, 5, 80),
-                          buckets=buckets)
+        return train_step(model, opt, [(z, x, y, m)], loss_fn, lr_fn(it), buckets=buckets)
+
+    step.graph_args = (model, opt, [(z, x, y, m)], loss_fn, lr_fn)
 
     return step, B * world, dict(workload=f"{kind}-caption-step", micro_batch=B, seq_len=31,
                                  grad_accum=1, global_batch=B * world)
@@ -130,15 +135,44 @@ def _quiet(fn):
         return fn()
 
 
-def timed(step, steps, warmup, world, timer=None):
+def graphed(step, warmup):
+    """Capture the step into one hipGraph (gvl.graph) after `warmup` eager steps."""
+    from gvl.graph import GraphedStep
+    model, opt, batches, loss_fn, lr_fn = step.graph_args
+    gs = GraphedStep(model, opt, batches, loss_fn, lr_fn(0), warmup=warmup)
+    return lambda it: gs(lr_fn(it))
+
+
+def kernel_pass(step, first_it, steps, timer):
+    """Per-GEMM HIP-event timing for the roofline line.  Events recorded while a hipGraph
+    is captured cannot time its replayed kernels on ROCm 7 (hipEventElapsedTime ->
+    hipErrorInvalidHandle; tools/probe_graph_events.py), so with graphs on, the same step
+    (same kernels, shapes and data) runs eagerly for `steps` steps with an event pair
+    around every GEMM launch on its stream; rocprofv3 sees both kinds of launch."""
     from gvl import kernels as K
-    for i in range(warmup):
-        step(i)
+    torch.cuda.synchronize()
+    K.set_kernel_timer(timer)
+    try:
+        for i in range(steps):
+            step(first_it + i)
+    finally:
+        K.set_kernel_timer(None)
+    torch.cuda.synchronize()
+
+
+def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
+    from gvl import kernels as K
+    eager = step
+    if graph:
+        step = graphed(step, warmup)
+    else:
+        for i in range(warmup):
+            step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if timer is not None:
+    if timer is not None and not graph:
         K.set_kernel_timer(timer)
     t0 = time.perf_counter()
     r = None
@@ -154,6 +188,8 @@ def timed(step, steps, warmup, world, timer=None):
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+    if graph and timer is not None:
+        kernel_pass(eager, warmup + steps, kernel_steps, timer)
     return dt, r
 
 
@@ -246,6 +282,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--caption-steps", type=int, default=10)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="eager steps (default at N=1: the step is captured into one hipGraph)")
     args = ap.parse_args()
 
     world, rank, dev = setup()
@@ -259,8 +297,9 @@ def main():
     else:
         step, units, cfg = run_caption(args.workload, args, world, rank, dev)
         unit, flop_per_unit = "images/s", CAP_FLOP_PER_IMAGE[args.workload]
+    use_graph = world == 1 and not args.no_graph
     timer = K.KernelTimer()
-    dt, res = timed(step, args.steps, args.warmup, world, timer)
+    dt, res = timed(step, args.steps, args.warmup, world, timer, graph=use_graph)
     value = units * args.steps / dt
     roof = dominant_kernel(timer.summary())
     out = {
@@ -272,6 +311,7 @@ def main():
         "config": dict(cfg, model="gpt2-124m", parallelism=f"dp{world}"),
         "step_mfma_frac": round(value * flop_per_unit / 1e12 / PEAK_BF16_TFLOPS / world, 4),
         "loss": round(float(res.loss), 5), "grad_norm": round(float(res.norm), 5),
+        "hip_graph": use_graph,
         "roofline": roof,
     }
     if args.workload == "lm" and not args.no_secondary:
@@ -279,7 +319,8 @@ def main():
         torch.cuda.empty_cache()
         cstep, cunits, ccfg = run_caption("qformer", args, world, rank, dev)
         ctimer = K.KernelTimer()
-        cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer)
+        cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer, graph=use_graph,
+                          kernel_steps=3)
         cval = cunits * args.caption_steps / cdt
         out["caption_qformer"] = dict(
             value=round(cval, 1), unit="images/s", ms_per_step=round(cdt / args.caption_steps * 1e3, 3),

@@ -37,6 +37,7 @@ struct AttnP {
   uint32_t drop_thresh;
   float drop_scale;
   uint64_t seed;
+  const uint64_t* seed_ptr;
 };
 
 struct AttnG {
@@ -106,6 +107,7 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 // ------------------------------------------------------------------------------------
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
           float pe = e;
           if constexpr (DROP) {
             const int64_t key = k0 + 16 * n + 4 * Gl + r;
-            pe = rng_keep(p.seed, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
+            pe = rng_keep(seed_, drow + (uint64_t)key, p.drop_thresh) ? e * p.drop_scale : 0.f;
           }
           sc[g][n][r] = pe;
         }
@@ -277,6 +279,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
 // dQ: block = (64*G-query tile, head, batch), each wave G groups of 16 query rows.
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
           if (msk && (kk >= kl || (p.causal && kk > ql))) pv = 0.f;
           float dpv = dp[g][n][r];
           if constexpr (DROP)
-            dpv = rng_keep(p.seed, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
+            dpv = rng_keep(seed_, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
           sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
         }
       sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
@@ -409,6 +412,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
 // 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int KB = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
   __shared__ __attribute__((aligned(16))) float sl[2][2][KT];         // [stage][lse2, D]
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg)
             float pdrop = pv, dpv = dp[g][n][r];
             if constexpr (DROP) {
               const bool keep = rng_keep(
-                  p.seed, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
+                  seed_, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
               pdrop = keep ? pv * p.drop_scale : 0.f;
               dpv = keep ? dpv * p.drop_scale : 0.f;
             }
@@ -595,6 +599,7 @@ int fill(const gvl_attn_desc* d, AttnP& p) {
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
   p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
   p.seed = d->seed;
+  p.seed_ptr = static_cast<const uint64_t*>(d->seed_ptr);
   return 0;
 }
 

@@ -101,6 +101,17 @@ GVL_DEV uint32_t rng_u32(uint64_t seed, uint64_t idx) {
   z ^= z >> 31;
   return (uint32_t)(z >> 32);
 }
+// Effective dropout seed: the call's seed, re-keyed by a device-side step offset when one is
+// given (graph replays advance the offset on the device, so a captured step draws fresh masks).
+GVL_DEV uint64_t seed_eff(uint64_t seed, const uint64_t* off) {
+  if (off == nullptr) return seed;
+  uint64_t z = *off;
+  if (z == 0) return seed;
+  z = (z + 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return seed ^ (z ^ (z >> 31));
+}
 // keep with probability 1-p: compare against threshold p * 2^32
 GVL_DEV bool rng_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
   return rng_u32(seed, idx) >= thresh;

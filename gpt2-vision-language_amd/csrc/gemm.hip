@@ -229,6 +229,7 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   p.ldr = d->ldr;
   p.gate = static_cast<const bf16_t*>(d->gate);
   p.seed = d->seed;
+  p.seed_ptr = static_cast<const uint64_t*>(d->seed_ptr);
   p.has_drop = d->drop_p > 0.f;
   p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);

@@ -18,6 +18,7 @@ struct GemmP {
   int64_t ldr;
   const bf16_t* gate;
   uint64_t seed;
+  const uint64_t* seed_ptr;
   float drop_scale;
   uint32_t drop_thresh;
   int tiles_m, tiles_n;
@@ -119,10 +120,11 @@ static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a,
         for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
       }
       if (p.has_drop) {
+        const uint64_t seed = seed_eff(p.seed, p.seed_ptr);
         const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          v[r] = rng_keep(p.seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
+          v[r] = rng_keep(seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
       }
       if (p.gate) {
         if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient

@@ -80,8 +80,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ p,
                                                     const bf16_t* __restrict__ g,
                                                     bf16_t* __restrict__ m, bf16_t* __restrict__ v,
                                                     int64_t n, int64_t n_decay, AdamP a,
-                                                    const float* __restrict__ gscale) {
+                                                    const float* __restrict__ gscale,
+                                                    const float* __restrict__ hyper) {
   const float cs = gscale ? *gscale : 1.f;
+  if (hyper) {  // device-resident {lr, step}: a captured step reads this step's values
+    a.lr = hyper[0];
+    a.bc1 = 1.f - powf(a.b1, hyper[1]);
+    a.bc2_sqrt = sqrtf(1.f - powf(a.b2, hyper[1]));
+  }
   const int64_t n8 = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
     float fp[8], fg[8], fm[8], fv[8];
@@ -177,8 +183,9 @@ int colsum_blocks(int64_t rows, int64_t* chunk) {
 __global__ __launch_bounds__(256) void dropout_apply_kernel(const bf16_t* __restrict__ in,
                                                             int64_t ldi, bf16_t* __restrict__ out,
                                                             int64_t ldo, int64_t rows, int64_t cols,
-                                                            uint64_t seed, uint32_t thresh,
-                                                            float scale) {
+                                                            uint64_t seed0, const uint64_t* seed_ptr,
+                                                            uint32_t thresh, float scale) {
+  const uint64_t seed = seed_eff(seed0, seed_ptr);
   const int64_t total = rows * cols;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
@@ -271,8 +278,27 @@ extern "C" int gvl_adamw(void* p, const void* g, void* m, void* v, int64_t n, in
   a.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   hipLaunchKernelGGL(adamw_kernel, dim3(ew_blocks(n >> 3)), dim3(256), 0, gvl::as_stream(stream),
                      static_cast<bf16_t*>(p), static_cast<const bf16_t*>(g),
-                     static_cast<bf16_t*>(m), static_cast<bf16_t*>(v), n, n_decay, a, grad_scale);
+                     static_cast<bf16_t*>(m), static_cast<bf16_t*>(v), n, n_decay, a, grad_scale,
+                     nullptr);
   GVL_LAUNCH_CHECK("gvl_adamw");
+  return 0;
+}
+
+extern "C" int gvl_adamw_dev(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
+                             const float* hyper, float beta1, float beta2, float eps,
+                             float weight_decay, const float* grad_scale, gvl_stream_t stream) {
+  GVL_REQUIRE(p && g && m && v && hyper, "gvl_adamw_dev: null buffer");
+  GVL_REQUIRE(gvl::aligned16(p) && gvl::aligned16(g) && gvl::aligned16(m) && gvl::aligned16(v),
+              "gvl_adamw_dev: arenas must be 16-byte aligned");
+  if (n == 0) return 0;
+  AdamP a;
+  a.lr = 0.f; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.bc1 = 1.f; a.bc2_sqrt = 1.f;
+  hipLaunchKernelGGL(adamw_kernel, dim3(ew_blocks(n >> 3)), dim3(256), 0, gvl::as_stream(stream),
+                     static_cast<bf16_t*>(p), static_cast<const bf16_t*>(g),
+                     static_cast<bf16_t*>(m), static_cast<bf16_t*>(v), n, n_decay, a, grad_scale,
+                     hyper);
+  GVL_LAUNCH_CHECK("gvl_adamw_dev");
   return 0;
 }
 
@@ -307,13 +333,14 @@ extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld,
 
 extern "C" int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_out,
                                       int64_t rows, int64_t cols, float p, uint64_t seed,
-                                      gvl_stream_t stream) {
+                                      const uint64_t* seed_ptr, gvl_stream_t stream) {
   GVL_REQUIRE(p >= 0.f && p < 1.f, "gvl_dropout_mask_apply: p out of range");
   if (rows * cols == 0) return 0;
   const uint32_t thresh = (uint32_t)((double)p * 4294967296.0);
   hipLaunchKernelGGL(dropout_apply_kernel, dim3(ew_blocks(rows * cols)), dim3(256), 0,
                      gvl::as_stream(stream), static_cast<const bf16_t*>(in), ld_in,
-                     static_cast<bf16_t*>(out), ld_out, rows, cols, seed, thresh, 1.f / (1.f - p));
+                     static_cast<bf16_t*>(out), ld_out, rows, cols, seed, seed_ptr, thresh,
+                     1.f / (1.f - p));
   GVL_LAUNCH_CHECK("gvl_dropout_mask_apply");
   return 0;
 }

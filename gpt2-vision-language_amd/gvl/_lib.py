@@ -35,6 +35,7 @@ class GemmDesc(C.Structure):
         ("drop_p", c_f32), ("seed", c_u64),
         ("c_fp32", c_i32),
         ("workspace", c_vp), ("workspace_bytes", c_i64),
+        ("seed_ptr", c_vp),
     ]
 
 
@@ -47,6 +48,7 @@ class AttnDesc(C.Structure):
         ("v_sb", c_i64), ("v_st", c_i64), ("v_sh", c_i64),
         ("o_sb", c_i64), ("o_st", c_i64), ("o_sh", c_i64),
         ("causal", c_i32), ("scale", c_f32), ("drop_p", c_f32), ("seed", c_u64),
+        ("seed_ptr", c_vp),
     ]
 
 
@@ -86,9 +88,11 @@ SIGNATURES = {
     "gvl_grad_norm": (C.c_int, [c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
     "gvl_adamw": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32,
                             c_f32, c_i64, c_vp, c_vp]),
+    "gvl_adamw_dev": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_f32, c_f32,
+                                c_f32, c_vp, c_vp]),
     "gvl_colsum_workspace_size": (c_i64, [c_i64, c_i64]),
     "gvl_colsum": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
-    "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64,
+    "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,
                                          c_vp]),
     "gvl_gate_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "gvl_gate_bwd_workspace_size": (c_i64, [c_i64]),

@@ -30,6 +30,11 @@ def new_seed():
     return int(torch.randint(1, 2**62, (1,)).item())
 
 
+def _off(t, p):
+    """Device dropout step offset (gvl.kernels.seed_offset) for a dropout site, else None."""
+    return K.seed_offset(t.device) if p > 0 else None
+
+
 def _need(ctx, i):
     return ctx.needs_input_grad[i]
 
@@ -165,7 +170,8 @@ class LinearFn(torch.autograd.Function):
         ybr = None
         if gate is not None:
             ybr = torch.empty(x2.shape[0], N, dtype=BF16, device=x.device)
-        y = K.linear(x2, w, b, residual=r2, gate=gate, pre_out=ybr, drop_p=drop_p, seed=seed)
+        y = K.linear(x2, w, b, residual=r2, gate=gate, pre_out=ybr, drop_p=drop_p, seed=seed,
+                     seed_ptr=_off(x2, drop_p))
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w, gate, ybr)
             ctx.cfg = (shp, N, drop_p, seed, residual is not None)
@@ -188,7 +194,7 @@ class LinearFn(torch.autograd.Function):
             if _need(ctx, 4):
                 dgate = gacc.to(gate.dtype).view_as(gate)
         if drop_p > 0:
-            dbr = K.dropout_mask_apply(dbr, drop_p, seed)
+            dbr = K.dropout_mask_apply(dbr, drop_p, seed, seed_ptr=_off(dbr, drop_p))
         dx = K.linear_dx(dbr, w).view(shp) if _need(ctx, 0) else None
         dw = K.linear_dw(dbr, x2) if _need(ctx, 1) else None
         db = K.colsum(dbr) if _need(ctx, 2) else None
@@ -206,7 +212,7 @@ class MLPFn(torch.autograd.Function):
         hpre = torch.empty(x2.shape[0], w1.shape[0], dtype=BF16, device=x.device)
         h = K.linear(x2, w1, b1, act=act, pre_out=hpre)
         r2 = residual.reshape(-1, w2.shape[0]).to(BF16).contiguous() if residual is not None else None
-        y = K.linear(h, w2, b2, residual=r2, drop_p=drop_p, seed=seed)
+        y = K.linear(h, w2, b2, residual=r2, drop_p=drop_p, seed=seed, seed_ptr=_off(h, drop_p))
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w1, w2, hpre, h)
             ctx.cfg = (shp, act, drop_p, seed, residual is not None)
@@ -219,7 +225,7 @@ class MLPFn(torch.autograd.Function):
         d2 = dy.reshape(-1, w2.shape[0]).to(BF16).contiguous()
         dres = dy if (has_res and _need(ctx, 5)) else None
         if drop_p > 0:
-            d2 = K.dropout_mask_apply(d2, drop_p, seed)
+            d2 = K.dropout_mask_apply(d2, drop_p, seed, seed_ptr=_off(d2, drop_p))
         dw2 = K.linear_dw(d2, h) if _need(ctx, 3) else None
         db2 = K.colsum(d2) if _need(ctx, 4) else None
         dpre = K.linear_dx(d2, w2, dact=act, pre_in=hpre)
@@ -260,9 +266,11 @@ class MHAFn(torch.autograd.Function):
             qv, kv_, vv = q3, k3[:, :, :C], k3[:, :, C:]
             qkv = None
         sa = seed ^ 0x5A5A5A5A
-        o, lse = K.attn_fwd(qv, kv_, vv, n_head, False, drop_p=p_attn, seed=sa)
+        o, lse = K.attn_fwd(qv, kv_, vv, n_head, False, drop_p=p_attn, seed=sa,
+                            seed_ptr=_off(qv, p_attn))
         r2 = residual.reshape(B * Tq, C).to(BF16).contiguous()
-        out = K.linear(o.view(B * Tq, C), out_w, out_b, residual=r2, drop_p=p_out, seed=seed)
+        out = K.linear(o.view(B * Tq, C), out_w, out_b, residual=r2, drop_p=p_out, seed=seed,
+                       seed_ptr=_off(o, p_out))
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse)
             ctx.cfg = (B, Tq, Tk, C, n_head, self_attn, p_attn, p_out, seed, sa)
@@ -274,7 +282,8 @@ class MHAFn(torch.autograd.Function):
         B, Tq, Tk, C, H, self_attn, p_attn, p_out, seed, sa = ctx.cfg
         d2 = dout.reshape(B * Tq, C).to(BF16).contiguous()
         dres = dout if _need(ctx, 6) else None
-        dbr = K.dropout_mask_apply(d2, p_out, seed) if p_out > 0 else d2
+        dbr = (K.dropout_mask_apply(d2, p_out, seed, seed_ptr=_off(d2, p_out)) if p_out > 0
+               else d2)
         d_out_w = K.linear_dw(dbr, o.view(B * Tq, C)) if _need(ctx, 4) else None
         d_out_b = K.colsum(dbr) if _need(ctx, 5) else None
         do = K.linear_dx(dbr, out_w).view(B, Tq, C)
@@ -287,7 +296,7 @@ class MHAFn(torch.autograd.Function):
             dp3 = dqkv.view(B, Tq, 3 * C)
             K.attn_bwd(do, p3[:, :, :C], p3[:, :, C:2 * C], p3[:, :, 2 * C:], o, lse, H, False,
                        dp3[:, :, :C], dp3[:, :, C:2 * C], dp3[:, :, 2 * C:], drop_p=p_attn,
-                       seed=sa)
+                       seed=sa, seed_ptr=_off(do, p_attn))
             if din_w is not None:
                 K.linear_dw(dqkv, q2, out=din_w)
             if din_b is not None:
@@ -301,7 +310,8 @@ class MHAFn(torch.autograd.Function):
             dkvp = torch.empty(B * Tk, 2 * C, dtype=BF16, device=d2.device)
             dk3 = dkvp.view(B, Tk, 2 * C)
             K.attn_bwd(do, q3, k3[:, :, :C], k3[:, :, C:], o, lse, H, False, dqp.view(B, Tq, C),
-                       dk3[:, :, :C], dk3[:, :, C:], drop_p=p_attn, seed=sa)
+                       dk3[:, :, :C], dk3[:, :, C:], drop_p=p_attn, seed=sa,
+                       seed_ptr=_off(do, p_attn))
             if din_w is not None:
                 K.linear_dw(dqp, q2, out=din_w[:C])
                 K.linear_dw(dkvp, kv2, out=din_w[C:])

@@ -90,10 +90,26 @@ def _gemm_workspace(device):
     return ws
 
 
+# ------------------------------------------------------------- device dropout offset
+_SEED_OFF = {}
+
+
+def seed_offset(device):
+    """Per-device int64 step offset that re-keys every dropout seed on the device
+    (include/gvl.h: seed_eff).  It stays 0 in eager use; gvl.graph advances it once per
+    replay of a captured step so frozen host seeds still draw fresh masks."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = _SEED_OFF.get(key)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=device)
+        _SEED_OFF[key] = t
+    return t
+
+
 # ------------------------------------------------------------------------------- GEMM
 def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, bias=None,
          act=0, dact=0, pre_out=None, pre_in=None, residual=None, gate=None, drop_p=0.0,
-         seed=0, out_dtype=BF16):
+         seed=0, seed_ptr=None, out_dtype=BF16):
     """C = epi(alpha * opA @ opB).  a: [M,K] (a_mn=False) or [K,M]; b: [N,K] (b_mn=False,
     nn.Linear weight) or [K,N].  Returns C [M,N]."""
     _dev(a, b)
@@ -126,6 +142,7 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     d.gate = _p(gate)
     d.drop_p = float(drop_p)
     d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    d.seed_ptr = _p(seed_ptr)
     d.c_fp32 = int(out.dtype == F32)
     ws = _gemm_workspace(a.device)
     d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
@@ -196,7 +213,7 @@ def _bthd(t, T, H):
     return t.stride(0), t.stride(1), 64
 
 
-def attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p=0.0, seed=0):
+def attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p=0.0, seed=0, seed_ptr=None):
     d = AttnDesc()
     d.q, d.k, d.v, d.o, d.lse = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), _p(lse)
     d.B, d.H, d.Tq, d.Tk = B, H, Tq, Tk
@@ -208,10 +225,11 @@ def attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p=0.0, seed=0):
     d.scale = float(scale)
     d.drop_p = float(drop_p)
     d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    d.seed_ptr = _p(seed_ptr)
     return d
 
 
-def attn_fwd(q, k, v, H, causal, scale=None, drop_p=0.0, seed=0, out=None):
+def attn_fwd(q, k, v, H, causal, scale=None, drop_p=0.0, seed=0, out=None, seed_ptr=None):
     """q: [B,Tq,*] view whose cols h*64.. are head h (e.g. a slice of packed qkv);
     k, v: [B,Tk,*].  Returns (o [B,Tq,H*64] bf16, lse [B,H,Tq] fp32)."""
     _dev(q, k, v)
@@ -225,18 +243,19 @@ def attn_fwd(q, k, v, H, causal, scale=None, drop_p=0.0, seed=0, out=None):
     if out is None:
         out = torch.empty(B, Tq, H * 64, dtype=BF16, device=q.device)
     lse = torch.empty(B, H, Tq, dtype=F32, device=q.device)
-    d = attn_desc(q, k, v, out, lse, B, H, Tq, Tk, causal, scale, drop_p, seed)
+    d = attn_desc(q, k, v, out, lse, B, H, Tq, Tk, causal, scale, drop_p, seed, seed_ptr)
     _lib.check(_L().gvl_attn_fwd(C.byref(d), _stream()), "gvl_attn_fwd")
     return out, lse
 
 
-def attn_bwd(dout, q, k, v, o, lse, H, causal, dq, dk, dv, scale=None, drop_p=0.0, seed=0):
+def attn_bwd(dout, q, k, v, o, lse, H, causal, dq, dk, dv, scale=None, drop_p=0.0, seed=0,
+             seed_ptr=None):
     """Writes dq/dk/dv (views with the layouts of q/k/v)."""
     B, Tq = q.shape[0], q.shape[1]
     Tk = k.shape[1]
     if scale is None:
         scale = 1.0 / math.sqrt(64)
-    d = attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p, seed)
+    d = attn_desc(q, k, v, o, lse, B, H, Tq, Tk, causal, scale, drop_p, seed, seed_ptr)
     g = AttnBwdDesc()
     g.dout, g.do_sb, g.do_st, g.do_sh = dout.data_ptr(), dout.stride(0), dout.stride(1), 64
     g.dq, g.dq_sb, g.dq_st, g.dq_sh = dq.data_ptr(), dq.stride(0), dq.stride(1), 64
@@ -321,6 +340,15 @@ def grad_norm(g_flat, max_norm, out=None):
     return out
 
 
+def adamw_dev(p, g, m, v, n_decay, hyper, beta1, beta2, eps, wd, grad_scale=None):
+    """AdamW with lr / step read on the device from hyper[0:2] (graph-capturable)."""
+    _dev(p, g, m, v, hyper)
+    _lib.check(_L().gvl_adamw_dev(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                  p.numel(), int(n_decay), hyper.data_ptr(), float(beta1),
+                                  float(beta2), float(eps), float(wd), _p(grad_scale), _stream()),
+               "gvl_adamw_dev")
+
+
 def adamw(p, g, m, v, n_decay, lr, beta1, beta2, eps, wd, step, grad_scale=None):
     _dev(p, g, m, v)
     _lib.check(_L().gvl_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
@@ -340,13 +368,14 @@ def colsum(x2, out=None, accumulate=False):
     return out
 
 
-def dropout_mask_apply(x2, p, seed, out=None):
+def dropout_mask_apply(x2, p, seed, out=None, seed_ptr=None):
     rows, cols = x2.shape
     if out is None:
         out = torch.empty(rows, cols, dtype=BF16, device=x2.device)
     _lib.check(_L().gvl_dropout_mask_apply(x2.data_ptr(), x2.stride(0), out.data_ptr(),
                                            out.stride(0), rows, cols, float(p),
-                                           int(seed) & 0xFFFFFFFFFFFFFFFF, _stream()),
+                                           int(seed) & 0xFFFFFFFFFFFFFFFF, _p(seed_ptr),
+                                           _stream()),
                "gvl_dropout_mask_apply")
     return out
 

@@ -73,6 +73,8 @@ class AdamW(torch.optim.Optimizer):
             st["exp_avg_sq"] = varena[o:o + n].view_as(p)
         self._arena = dict(p=parena, g=garena, m=marena, v=varena, offs=offs, seg=seg,
                            params=params)
+        # per group {lr, step} on the device, read by the AdamW kernel (capturable step)
+        self._hyper = torch.zeros(len(self.param_groups), 2, dtype=torch.float32, device=dev)
 
     @property
     def grad_arena(self):
@@ -119,25 +121,43 @@ class AdamW(torch.optim.Optimizer):
         self._clip_coef = out[1:2]
         return out[0]
 
+    def stage_hyper(self):
+        """Copy each group's current lr and the step count to the device block the AdamW
+        kernel reads (pinned host buffer, stream-ordered, no host sync)."""
+        vals = torch.tensor([[float(g["lr"]), float(self._step_count)] for g in self.param_groups],
+                            dtype=torch.float32).pin_memory()
+        self._hyper.copy_(vals, non_blocking=True)
+
+    def advance(self):
+        """Host side of one optimizer step: bump the step count and stage {lr, step}.
+        step() does this itself; a replayed hipGraph (gvl.graph) calls it per replay."""
+        self._step_count += 1
+        self.stage_hyper()
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         if self._arena is None:
             self._build()
         self._sync_grads()
-        self._step_count += 1
+        if not torch.cuda.is_current_stream_capturing():
+            self.advance()
         a = self._arena
-        for g, (s0, s1) in zip(self.param_groups, a["seg"]):
+        for gi, (g, (s0, s1)) in enumerate(zip(self.param_groups, a["seg"])):
             if s1 == s0:
                 continue
             b1, b2 = g["betas"]
-            K.adamw(a["p"][s0:s1], a["g"][s0:s1], a["m"][s0:s1], a["v"][s0:s1], s1 - s0,
-                    g["lr"], b1, b2, g["eps"], g["weight_decay"], self._step_count,
-                    grad_scale=self._clip_coef)
-        for p in a["params"]:
-            self.state[p]["step"].fill_(self._step_count)
+            K.adamw_dev(a["p"][s0:s1], a["g"][s0:s1], a["m"][s0:s1], a["v"][s0:s1], s1 - s0,
+                        self._hyper[gi], b1, b2, g["eps"], g["weight_decay"],
+                        grad_scale=self._clip_coef)
         self._clip_coef = None
         return loss
+
+    def state_dict(self):
+        if self._arena is not None:
+            for p in self._arena["params"]:
+                self.state[p]["step"].fill_(self._step_count)
+        return super().state_dict()
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)

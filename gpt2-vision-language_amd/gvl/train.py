@@ -48,8 +48,9 @@ def train_step(model, optimizer, micro_batches, loss_fn, lr, *, buckets: GradBuc
         buckets.wait()
     all_reduce_mean_(loss_accum, process_group)
     norm = clip_grad_norm_(optimizer, max_norm)
-    for g in optimizer.param_groups:
-        g["lr"] = lr
+    if lr is not None:  # None: keep the groups' lr (a captured step stages it per replay)
+        for g in optimizer.param_groups:
+            g["lr"] = lr
     optimizer.step()
     return StepResult(loss_accum, norm)
 

@@ -26,7 +26,13 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 1
+#define GVL_ABI_VERSION 2
+
+/* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
+ * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
+ * A training step captured into a hipGraph keeps its host seeds frozen; advancing the
+ * device-side offset once per replay gives every step fresh masks (forward and backward
+ * of one step read the same offset, so they agree). */
 
 typedef void* gvl_stream_t;
 
@@ -67,6 +73,7 @@ typedef struct gvl_gemm_desc {
   int32_t c_fp32;         /* 1: C is fp32 */
   void* workspace;        /* optional fp32 scratch for split-K (few output tiles, long K) */
   int64_t workspace_bytes;
+  const uint64_t* seed_ptr; /* optional device step offset re-keying `seed` (see below) */
 } gvl_gemm_desc;
 int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests): impl 1 = LDS-DMA
@@ -118,6 +125,7 @@ typedef struct gvl_attn_desc {
   float scale;
   float drop_p;
   uint64_t seed;
+  const uint64_t* seed_ptr; /* optional device step offset re-keying `seed` */
 } gvl_attn_desc;
 int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream);
 /* Backward: dO has the layout of o (do_* strides); dq/dk/dv the layouts of q/k/v
@@ -187,6 +195,12 @@ int gvl_grad_norm(const void* g, int64_t n, float max_norm, void* workspace, flo
 int gvl_adamw(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
               float lr, float beta1, float beta2, float eps, float weight_decay,
               int64_t step, const float* grad_scale, gvl_stream_t stream);
+/* As gvl_adamw with lr and the 1-based step read on the device from hyper[0], hyper[1]
+ * (fp32): a step captured into a hipGraph stays correct across replays when the caller
+ * advances `hyper` (param_groups[i]['lr'] written before each step, train_gpt2.py:474-476). */
+int gvl_adamw_dev(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
+                  const float* hyper, float beta1, float beta2, float eps, float weight_decay,
+                  const float* grad_scale, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Small fused elementwise helpers on the hot path. */
@@ -199,7 +213,7 @@ int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
  * same counter-based mask the GEMM epilogue applies. */
 int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_out,
                            int64_t rows, int64_t cols, float p, uint64_t seed,
-                           gvl_stream_t stream);
+                           const uint64_t* seed_ptr, gvl_stream_t stream);
 /* out[i] = tanh(*gate) * in[i] and gate_grad (fp32 scalar, accumulated) +=
  * (1 - tanh^2) * sum_i in[i] * y[i] — backward of x + tanh(g) * y
  * (gpt2_cross-att/model.py:101). */

@@ -1,0 +1,91 @@
+"""Time every GEMM shape of the LM and Q-Former steps: libgvl (default pick and forced
+configs) next to torch.mm (hipBLASLt) as a yardstick.  One process, HIP events.
+python tools/gemm_shapes.py [lm|qf|all] [cfgs comma list, -1 = default pick]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "gpt2-vision-language_amd"))
+from gvl import _lib  # noqa: E402
+from gvl import kernels as K  # noqa: E402
+
+T = 16384  # LM tokens per micro-step
+Q = 8064   # Q-Former caption rows (128 x 63)
+QT = 3968  # caption text rows (128 x 31)
+# (name, M, N, K, a_mn, b_mn)
+LM = [
+    ("c_attn", T, 2304, 768, 0, 0), ("attn.c_proj", T, 768, 768, 0, 0),
+    ("c_fc", T, 3072, 768, 0, 0), ("mlp.c_proj", T, 768, 3072, 0, 0),
+    ("lm_head", T, 50304, 768, 0, 0),
+    ("c_attn.dX", T, 768, 2304, 0, 1), ("attn.c_proj.dX", T, 768, 768, 0, 1),
+    ("c_fc.dX", T, 768, 3072, 0, 1), ("mlp.c_proj.dX", T, 3072, 768, 0, 1),
+    ("lm_head.dX", T, 768, 50304, 0, 1),
+    ("c_attn.dW", 2304, 768, T, 1, 1), ("attn.c_proj.dW", 768, 768, T, 1, 1),
+    ("c_fc.dW", 3072, 768, T, 1, 1), ("mlp.c_proj.dW", 768, 3072, T, 1, 1),
+    ("lm_head.dW", 50304, 768, T, 1, 1),
+]
+QF = [
+    ("q.c_attn", Q, 2304, 768, 0, 0), ("q.c_proj", Q, 768, 768, 0, 0),
+    ("q.c_fc", Q, 3072, 768, 0, 0), ("q.mlp.c_proj", Q, 768, 3072, 0, 0),
+    ("q.lm_head", Q, 50304, 768, 0, 0),
+    ("q.lm_head.dX", QT, 768, 50304, 0, 1),
+    ("q.c_attn.dX", Q, 768, 2304, 0, 1), ("q.c_fc.dX", Q, 768, 3072, 0, 1),
+    ("q.mlp.c_proj.dX", Q, 3072, 768, 0, 1), ("q.c_proj.dX", Q, 768, 768, 0, 1),
+]
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1]
+    shapes = (LM if which in ("lm", "all") else []) + (QF if which in ("qf", "all") else [])
+    L = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    tot = {}
+    for name, M, N, Kd, am, bm in shapes:
+        A = (torch.randn(Kd, M, device="cuda", generator=g) if am else
+             torch.randn(M, Kd, device="cuda", generator=g)).bfloat16()
+        B = (torch.randn(Kd, N, device="cuda", generator=g) if bm else
+             torch.randn(N, Kd, device="cuda", generator=g)).bfloat16()
+        C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        fl = 2.0 * M * N * Kd
+        row = [f"{name:16s} {M:6d}x{N:6d}x{Kd:6d} {'tn'[am]}{'tn'[bm]}"]
+        ref = None
+        for cfg in cfgs + [99]:
+            if cfg == 99:
+                at = A.t() if am else A
+                bt = B if bm else B.t()
+                fn = lambda: torch.mm(at, bt, out=C)  # noqa: E731
+            else:
+                L.gvl_gemm_tune(2, cfg)
+                fn = lambda: K.gemm(A, B, a_mn=bool(am), b_mn=bool(bm), out=C)  # noqa: E731
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            if cfg == -1:
+                ref = C.float().clone()
+            elif ref is not None:
+                err = (C.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-9)
+                if err > 2e-2:
+                    row.append(f"MISMATCH({err:.3g})")
+            iters = max(3, min(50, int(2e12 / fl)))
+            e0, e1 = ev(), ev()
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / iters * 1e3
+            tf = fl / us / 1e6
+            tot.setdefault(cfg, 0.0)
+            tot[cfg] += us
+            row.append(f"{'torch' if cfg == 99 else 'cfg' + str(cfg)}:{us:8.1f}us {tf:6.0f}TF")
+        print(" ".join(row), flush=True)
+        del A, B, C
+    print("totals(us):", {k: round(v, 1) for k, v in tot.items()}, flush=True)
+    L.gvl_gemm_tune(2, -1)
+
+
+if __name__ == "__main__":
+    main()
