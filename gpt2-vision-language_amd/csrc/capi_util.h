@@ -8,6 +8,7 @@
 namespace gvl {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+int num_cus();  // compute units of the current device (cached per device)
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }

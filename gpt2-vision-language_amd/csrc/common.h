@@ -17,8 +17,11 @@ GVL_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
   return __builtin_bit_cast(bf16_t, b);
 }
-GVL_DEV uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+GVL_DEV uint32_t pack2(float lo, float hi) {  // one v_cvt_pk_bf16_f32 (RNE)
+  const bf16x2_t b = __builtin_convertvector(float2_t{lo, hi}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, b);
 }
 GVL_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 GVL_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }

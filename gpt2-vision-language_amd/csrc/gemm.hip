@@ -148,10 +148,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
   gemm_epilogue<4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-// GVL_GEMM_IMPL=regstage|lds|ring picks the kernel family (0|1|2); GVL_GEMM_CFG=0..3 forces
-// a tile config of that family.
+// GVL_GEMM_IMPL=regstage|lds|ring|pp picks the kernel family (0|1|2|3, default 3: the
+// persistent ping-pong kernel where it fills the chip, else the 128x128 ring);
+// GVL_GEMM_CFG forces a tile config of that family.
 struct GemmEnv {
-  int impl = 2, cfg = -1, group = 8;
+  int impl = 3, cfg = -1, group = 8;
   GemmEnv() {
     const char* gr = getenv("GVL_GEMM_GROUP");
     if (gr && atoi(gr) > 0) group = atoi(gr);
@@ -159,6 +160,7 @@ struct GemmEnv {
     if (s && s[0] == 'r' && s[1] == 'e') impl = 0;
     if (s && s[0] == 'l') impl = 1;
     if (s && s[0] == 'r' && s[1] == 'i') impl = 2;
+    if (s && s[0] == 'p') impl = 3;
     const char* c = getenv("GVL_GEMM_CFG");
     if (c) cfg = atoi(c);
   }
@@ -168,10 +170,39 @@ GemmEnv& env() {
   return e;
 }
 
+void fill_params(const gvl_gemm_desc* d, GemmP& p) {
+  p.A = static_cast<const bf16_t*>(d->a);
+  p.B = static_cast<const bf16_t*>(d->b);
+  p.C = d->c;
+  p.M = d->m; p.N = d->n; p.K = d->k;
+  p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
+  p.alpha = d->alpha;
+  p.alpha_ptr = d->alpha_ptr;
+  p.bias = static_cast<const bf16_t*>(d->bias);
+  p.pre_out = static_cast<bf16_t*>(d->pre_out);
+  p.pre_in = static_cast<const bf16_t*>(d->pre_in);
+  p.ldp = d->ldp;
+  p.residual = static_cast<const bf16_t*>(d->residual);
+  p.ldr = d->ldr;
+  p.gate = static_cast<const bf16_t*>(d->gate);
+  p.seed = d->seed;
+  p.seed_ptr = static_cast<const uint64_t*>(d->seed_ptr);
+  p.has_drop = d->drop_p > 0.f;
+  p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
+  p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
+  p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
+  p.splits = 1;
+  p.kper = d->k;
+  p.group = env().group;
+  p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
+             ? static_cast<float*>(d->workspace) : nullptr;
+  p.ws_bytes = p.ws ? d->workspace_bytes : 0;
+}
+
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 2 && cfg >= -1 && cfg <= 5, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 5, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -180,7 +211,21 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
-  if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
+  if (env().impl == 3 && gvl::gemm_ring_ok(d)) {
+    GemmP p;
+    fill_params(d, p);
+    if (env().cfg >= 0) {
+      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg), tf[d->a_mn != 0],
+               tf[d->b_mn != 0]);
+    } else if (gvl::gemm_pp3_plan(p, false)) {
+      const char* epi[6] = {"0", "1", "2", "3", "4", "5"};
+      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
+               epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)]);
+    } else {
+      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1)),
+               tf[d->a_mn != 0], tf[d->b_mn != 0]);
+    }
+  } else if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
     const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
     snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(cfg), tf[d->a_mn != 0], tf[d->b_mn != 0]);
   } else if (env().impl >= 1 && gvl::gemm_lds_ok(d)) {
@@ -214,33 +259,17 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GVL_REQUIRE(!d->residual || d->ldr % 4 == 0, "gvl_gemm: ldr must be a multiple of 4");
   GVL_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "gvl_gemm: drop_p out of range");
   GemmP p;
-  p.A = static_cast<const bf16_t*>(d->a);
-  p.B = static_cast<const bf16_t*>(d->b);
-  p.C = d->c;
-  p.M = d->m; p.N = d->n; p.K = d->k;
-  p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
-  p.alpha = d->alpha;
-  p.alpha_ptr = d->alpha_ptr;
-  p.bias = static_cast<const bf16_t*>(d->bias);
-  p.pre_out = static_cast<bf16_t*>(d->pre_out);
-  p.pre_in = static_cast<const bf16_t*>(d->pre_in);
-  p.ldp = d->ldp;
-  p.residual = static_cast<const bf16_t*>(d->residual);
-  p.ldr = d->ldr;
-  p.gate = static_cast<const bf16_t*>(d->gate);
-  p.seed = d->seed;
-  p.seed_ptr = static_cast<const uint64_t*>(d->seed_ptr);
-  p.has_drop = d->drop_p > 0.f;
-  p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
-  p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
-  p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
-  p.splits = 1;
-  p.kper = d->k;
-  p.group = env().group;
-  p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
-             ? static_cast<float*>(d->workspace) : nullptr;
-  p.ws_bytes = p.ws ? d->workspace_bytes : 0;
+  fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
+  if (env().impl == 3 && gvl::gemm_ring_ok(d)) {
+    if (env().cfg >= 0) {
+      gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg, s);
+    } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
+      gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1), s);
+    }
+    GVL_LAUNCH_CHECK("gvl_gemm(pp)");
+    return 0;
+  }
   if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
     const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
     gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, cfg, s);

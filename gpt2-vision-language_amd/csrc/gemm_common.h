@@ -94,57 +94,144 @@ GVL_DEV void gemm_epilogue(const GemmP& p, const float4_t (&acc)[FM][FN], int64_
   }
 }
 
-static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a, int64_t m,
-                                                        int64_t n, float alpha, float gatev) {
-  {
-    {
-      float v[4];
+// Fused epilogue math for one 4-column group (row m, cols n..n+3) -> the 4 output values
+// in fp32 (side outputs — pre-activation / un-gated branch — are stored here).
+static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a, int64_t m,
+                                                        int64_t n, float alpha, float gatev,
+                                                        float (&v)[4]) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
-      if (p.bias) {
-        const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
-        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
-      }
-      if (p.dact) {
-        const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
-        const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
+  for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
+  if (p.bias) {
+    const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
+    v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+  }
+  if (p.dact) {
+    const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
+    const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
-      }
-      if (p.act) {
-        if (p.pre_out) {
-          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
+    for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+  }
+  if (p.act) {
+    if (p.pre_out) {
+      *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
-      }
-      if (p.has_drop) {
-        const uint64_t seed = seed_eff(p.seed, p.seed_ptr);
-        const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
+    for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
+  }
+  if (p.has_drop) {
+    const uint64_t seed = seed_eff(p.seed, p.seed_ptr);
+    const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = rng_keep(seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
-      }
-      if (p.gate) {
-        if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient
-          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
+    for (int r = 0; r < 4; ++r)
+      v[r] = rng_keep(seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
+  }
+  if (p.gate) {
+    if (p.pre_out && !p.act) {  // save the un-gated branch for the gate gradient
+      *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
+          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= gatev;
-      }
-      if (p.residual) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
-        v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
-      }
-      if (p.c_f32) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + m * p.ldc + n) =
-            make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+    for (int r = 0; r < 4; ++r) v[r] *= gatev;
+  }
+  if (p.residual) {
+    const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
+    v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+  }
+}
+
+// Compile-time epilogue kinds for the persistent kernels (gemm_pp2.hip): each instance
+// carries only its own ops; EPI_GEN runs the runtime-flag path above.
+enum { EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5 };
+
+template <int EPI>
+static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t a, int64_t m,
+                                                          int64_t n, float alpha, float gatev,
+                                                          float (&v)[4]) {
+  if constexpr (EPI == EPI_GEN) {
+    gemm_epi_vals(p, a, m, n, alpha, gatev, v);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_ACT) {
+      const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
+      v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+    }
+    if constexpr (EPI == EPI_DACT) {
+      const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
+      const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+    }
+    if constexpr (EPI == EPI_BIAS_ACT) {
+      if (p.pre_out) {
+        *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
             make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
+    }
+    if constexpr (EPI == EPI_BIAS_RES) {
+      const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
+      v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+    }
+  }
+}
+
+static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a, int64_t m,
+                                                        int64_t n, float alpha, float gatev) {
+  float v[4];
+  gemm_epi_vals(p, a, m, n, alpha, gatev, v);
+  if (p.c_f32) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + m * p.ldc + n) =
+        make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+        make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  }
+}
+
+// bf16-output epilogue with 16-byte stores (needs N % 8 == 0, ldc % 8 == 0, FN even).
+// For fragment pair (j, j+1) a lane of column quad q holds 4 columns of each; two
+// v_permlane16_swap_b32 (lanes l <-> l^16 across the pair) leave every lane 8 consecutive
+// columns: quad q stores cols 16 (j + (q & 1)) + 8 (q >> 1) .. + 7, so one store
+// instruction writes 16 rows x 64 B instead of 16 rows x 32 B.
+template <int FM, int FN, int EPI = EPI_GEN>
+GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
+                             int64_t nw0, int lane, float alpha) {
+  static_assert(FN % 2 == 0, "fragment pairs");
+  float gatev = 1.f;
+  if constexpr (EPI == EPI_GEN) gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
+  const bool plain = EPI == EPI_PLAIN ||
+                     (EPI == EPI_GEN && !p.bias && !p.dact && !p.act && !p.has_drop && !p.gate &&
+                      !p.residual);
+  const int q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t m = mw0 + i * 16 + (lane & 15);
+    const bool mok = m < p.M;
+#pragma unroll
+    for (int j = 0; j < FN; j += 2) {
+      const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
+      uint32_t x0, y0, x1, y1;  // packed bf16 pairs: frag j (x0: cols 0-1, y0: 2-3), frag j+1
+      if (plain) {
+        x0 = pack2(acc[i][j][0] * alpha, acc[i][j][1] * alpha);
+        y0 = pack2(acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+        x1 = pack2(acc[i][j + 1][0] * alpha, acc[i][j + 1][1] * alpha);
+        y1 = pack2(acc[i][j + 1][2] * alpha, acc[i][j + 1][3] * alpha);
+      } else {
+        float v0[4] = {0.f, 0.f, 0.f, 0.f}, v1[4] = {0.f, 0.f, 0.f, 0.f};
+        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, v0);
+        if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, v1);
+        x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
+        x1 = pack2(v1[0], v1[1]); y1 = pack2(v1[2], v1[3]);
+      }
+      const auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
+      const int64_t n = nw0 + 16 * (j + (q & 1)) + 8 * (q >> 1);
+      if (mok && n < p.N)
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
+            make_uint4(sx[0], sy[0], sx[1], sy[1]);
     }
   }
 }
@@ -177,4 +264,10 @@ const char* gemm_ring_name(int cfg);
 bool gemm_ring_ok(const gvl_gemm_desc* d);
 int gemm_ring_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
 int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced);
+const char* gemm_pp2_name(int cfg);
+int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
+int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels
+bool gemm_pp3_plan(GemmP& p, bool force);
+bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
+int gemm_pp3_splits(int64_t M, int64_t N, int64_t K);
 }  // namespace gvl

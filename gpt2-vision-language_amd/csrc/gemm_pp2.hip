@@ -1,0 +1,433 @@
+// bf16 GEMM v4: ping-pong 256x256 with whole-tile clusters.
+//
+// The v3 ping-pong (gemm_ring.hip, gemm_pp_kernel) splits every 32-deep K-step into two
+// row halves, so each barrier-delimited cluster holds 16 MFMAs (256 cycles of the SIMD's
+// matrix pipe) while the partner wave's memory cluster (8 ds_read_b128, or 4 reads + the
+// step's 4 LDS-DMA issues) often runs longer: the matrix pipe idles at every other barrier.
+// Here a cluster is KC whole K-steps of the wave's 128x64 output: 32*KC MFMAs against a
+// memory cluster of 12*KC fragment reads + 4*KC DMA issues, and one barrier pair per
+// cluster instead of per half step.
+//
+// Waves: group g = wave / 4 (output rows 128 g ..), column block wc = wave % 4 (64 cols);
+// group 1 runs one barrier behind group 0, so on every SIMD one wave computes while the
+// other loads.  Phase 2c: group 0 M(c), group 1 C(c-1); phase 2c+1: group 0 C(c), group 1
+// M(c).  LDS ring of NS slots of 32-deep K-steps (A[256][32] + B[256][32] = 32 KiB each).
+//  * M(c) reads cluster c's fragments and issues the DMA of steps [cKC+NS-KC, cKC+NS) into
+//    cluster c-1's slots: their last readers (group 1's M(c-1), phase 2c-1) retired their
+//    reads (lgkmcnt(0)) before the barrier closing phase 2c-1;
+//  * cluster c+1's steps are retired (counted vmcnt) by every wave before the barrier that
+//    closes phase 2c+1: group 1 at the end of M(c), group 0 at the end of C(c).
+#include "common.h"
+#include "capi_util.h"
+#include "gemm_common.h"
+#include "gemm_ring.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+using namespace gvl_ring;
+
+template <int NS, int KC, bool AMN, bool BMN>
+__global__ __launch_bounds__(512, 1) void gemm_pp2_kernel(GemmP p) {
+  constexpr int BM = 256, BN = 256, NW = 8, FM = 8, FN = 4;
+  static_assert(NS >= 2 * KC && NS <= 5, "ring geometry");
+  using SA = Step<BM, AMN, NW>;
+  using SB = Step<BN, BMN, NW>;
+  constexpr int SLOT = SA::BYTES + SB::BYTES;
+  constexpr int IPW = (SA::NINSTR + SB::NINSTR) / NW;
+  constexpr int INFL = NS - 2 * KC;  // steps left in flight across the cluster barrier
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wave >> 2, wc = wave & 3;
+
+  int split, tm, tn;
+  gemm_work_tile(p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * p.kper;
+  const int64_t kend = kbeg + p.kper < p.K ? kbeg + p.kper : p.K;
+  const int nks = (int)((kend - kbeg) / KS);
+  const int ncl = (nks + KC - 1) / KC;
+
+  const int64_t a_rows = AMN ? p.K : p.M, b_rows = BMN ? p.K : p.N;
+  const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
+  auto issue = [&](int ks) {
+    if (ks < nks) {
+      char* slot = smem + (ks % NS) * SLOT;
+      const int64_t k0 = kbeg + (int64_t)ks * KS;
+      SA::issue(ra, p.lda, m0, k0, slot, wave, lane);
+      SB::issue(rb, p.ldb, n0, k0, slot + SA::BYTES, wave, lane);
+    }
+  };
+  // steps issued but not needed by cluster c+1, after M(c)'s issue: min(INFL, nks - (c+2)KC)
+  auto inflight_after = [&](int c) {
+    const int r = nks - (c + 2) * KC;
+    return r < 0 ? 0 : (r < INFL ? r : INFL);
+  };
+
+  float4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int arow = g * 128, bcol = wc * 64;
+#pragma unroll
+  for (int i = 0; i < NS - KC; ++i) issue(i);
+  {  // cluster 0 retired: of steps [0, NS-KC) leave min(NS-2KC, nks-KC) in flight
+    const int r = nks - KC;
+    wait_vm_steps<IPW, (INFL > 0 ? INFL : 0)>(r < 0 ? 0 : (r < INFL ? r : INFL));
+  }
+  barrier_lds();
+  if (g == 1) __builtin_amdgcn_s_barrier();
+
+  short8_t af[KC][FM], bf[KC][FN];
+  for (int c = 0; c < ncl; ++c) {
+    // ---- M(c): fragments of cluster c, DMA of the steps refilling cluster c-1's slots
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      const int s = c * KC + q;
+      const char* sl = smem + (s % NS) * SLOT;
+      if (s < nks) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[q][j] = SB::frag(sl + SA::BYTES, bcol + 16 * j, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[q][i] = SA::frag(sl, arow + 16 * i, lane);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) issue(c * KC + NS - KC + q);
+    if (g == 1) wait_vm_steps<IPW, (INFL > 0 ? INFL : 0)>(inflight_after(c));
+    barrier_lds();
+    // ---- C(c)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      if (c * KC + q < nks) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[q][j], af[q][i], acc[i][j]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (g == 0) wait_vm_steps<IPW, (INFL > 0 ? INFL : 0)>(inflight_after(c));
+    barrier_lds();
+  }
+  if (g == 0) __builtin_amdgcn_s_barrier();
+
+  if (p.splits > 1) {
+    gemm_store_partial<FM, FN>(p, acc, split, m0 + arow, n0 + bcol, lane);
+  } else {
+    gemm_epilogue<FM, FN>(p, acc, m0 + arow, n0 + bcol, lane);
+  }
+}
+
+template <int NS, int KC, bool AMN, bool BMN>
+int launch_pp2(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_m = (int)((p.M + 255) / 256);
+  p.tiles_n = (int)((p.N + 255) / 256);
+  constexpr int lds = NS * 512 * KS * 2;
+  auto kern = gemm_pp2_kernel<NS, KC, AMN, BMN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  p.splits = 1;
+  if (p.ws != nullptr) {
+    const int sp = gvl::gemm_splitk_pick((int64_t)p.tiles_m * p.tiles_n, p.K);
+    if (sp > 1 && (int64_t)sp * p.M * p.N * 4 <= p.ws_bytes) p.splits = sp;
+  }
+  p.kper = p.splits > 1 ? ((p.K / p.splits + KS - 1) / KS) * KS : p.K;
+  if (p.splits > 1) p.splits = (int)((p.K + p.kper - 1) / p.kper);
+  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(512), lds, s, p);
+  if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
+  return 0;
+}
+
+// Persistent variant (v5): grid = min(tiles, CUs); workgroup b walks tiles b, b+G, b+2G..
+// and the LDS ring runs straight across tile boundaries (the next tile's first K-steps are
+// already landing while the current tile finishes), so no tile pays a cold prologue.  A
+// tile's epilogue runs at the start of the next memory cluster M(c), i.e. while the partner
+// wave of the SIMD is in its compute cluster; its 16-B stores drain behind the following
+// MFMAs.  (vmcnt waits stay correct: stores and loads retire in issue order, so a counted
+// wait for K-step c+1 at most also waits for part of the stores issued after it.)
+// DMA addresses: per-lane offsets are computed once per tile; a K-step only adds a scalar
+// soffset.  The epilogue kind EPI is a template parameter so the loop carries only its ops.
+// Split-K: work item w = (tile w / splits, K-slice w % splits), every slice kper deep (the
+// host only splits when K divides evenly); slices store fp32 partials, gemm_splitk_reduce
+// applies the epilogue.  KC = 1, bf16 output.
+template <int NS, bool AMN, bool BMN, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
+  constexpr int BM = 256, BN = 256, NW = 8, FM = 8, FN = 4;
+  static_assert(NS >= 3 && NS <= 5, "ring geometry");
+  using SA = Step<BM, AMN, NW>;
+  using SB = Step<BN, BMN, NW>;
+  constexpr int SLOT = SA::BYTES + SB::BYTES;
+  constexpr int IPW = (SA::NINSTR + SB::NINSTR) / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wave >> 2, wc = wave & 3;
+
+  const int total = p.tiles_m * p.tiles_n * p.splits;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int ntl = (total - b + G - 1) / G;  // work items of this workgroup
+  const int nks = (int)(p.kper / KS);
+  const int nsteps = ntl * nks;
+  // work item of local item t: XCD-contiguous remap over the virtual grid of `total` items
+  // (G % 8 == 0 keeps b + tG on workgroup b's XCD), then the L2-grouped walk
+  auto tile_coords = [&](int t, int64_t& m0, int64_t& n0, int64_t& k0, int& split) {
+    const int vid = b + t * G;
+    const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
+    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
+    int tm, tn;
+    gemm_tile_of(work, p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
+    m0 = (int64_t)tm * BM;
+    n0 = (int64_t)tn * BN;
+    k0 = (int64_t)split * p.kper;
+  };
+
+  const int64_t a_rows = AMN ? p.K : p.M, b_rows = BMN ? p.K : p.N;
+  const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
+  const int sa_step = SA::step_bytes(p.lda), sb_step = SB::step_bytes(p.ldb);
+  // issue cursor (steps are issued strictly in order)
+  int is_t = 0, is_k = 0;
+  int offa[SA::PER], offb[SB::PER];
+  {
+    int64_t m0, n0, k0;
+    int sp;
+    tile_coords(0, m0, n0, k0, sp);
+    SA::base_offsets(p.lda, m0, k0, wave, lane, offa);
+    SB::base_offsets(p.ldb, n0, k0, wave, lane, offb);
+  }
+
+#define GVL_PP3_ISSUE(gstep)                                                        \
+  do {                                                                              \
+    if ((gstep) < nsteps) {                                                         \
+      char* slot_ = smem + ((gstep) % NS) * SLOT;                                   \
+      SA::issue_at(ra, offa, is_k * sa_step, slot_, wave);                          \
+      SB::issue_at(rb, offb, is_k * sb_step, slot_ + SA::BYTES, wave);              \
+      if (++is_k == nks) {                                                          \
+        is_k = 0;                                                                   \
+        if (++is_t < ntl) {                                                         \
+          int64_t m0_, n0_, k0_;                                                    \
+          int sp_;                                                                  \
+          tile_coords(is_t, m0_, n0_, k0_, sp_);                                    \
+          SA::base_offsets(p.lda, m0_, k0_, wave, lane, offa);                      \
+          SB::base_offsets(p.ldb, n0_, k0_, wave, lane, offb);                      \
+        }                                                                           \
+      }                                                                             \
+    }                                                                               \
+  } while (0)
+
+  float4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int arow = g * 128, bcol = wc * 64;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) GVL_PP3_ISSUE(i);
+  {
+    const int r = nsteps - 1;
+    wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+  }
+  barrier_lds();
+  if (g == 1) __builtin_amdgcn_s_barrier();
+
+  // alpha (x *alpha_ptr, a device scalar written before this launch) read once up front: a
+  // load inside the loop would make hipcc drain the DMA queue (vmcnt(0)) at every epilogue
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  int cu_t = 0, cu_k = 0;  // compute cursor
+  int64_t cu_m0, cu_n0, cu_k0;
+  int cu_sp;
+  tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp);
+#define GVL_PP3_EPILOGUE()                                                                   \
+  do {                                                                                       \
+    if (p.splits > 1)                                                                        \
+      gemm_store_partial<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane);           \
+    else                                                                                     \
+      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha);         \
+  } while (0)
+
+  short8_t af[FM], bf[FN];
+  for (int c = 0; c < nsteps; ++c) {
+    // ---- M(c): previous tile's epilogue, fragments of step c, DMA of step c+NS-1
+    if (cu_k == 0 && c > 0) {
+      GVL_PP3_EPILOGUE();
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+      ++cu_t;
+      tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp);
+    }
+    const char* sl = smem + (c % NS) * SLOT;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf[j] = SB::frag(sl + SA::BYTES, bcol + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = SA::frag(sl, arow + 16 * i, lane);
+    GVL_PP3_ISSUE(c + NS - 1);
+    {
+      const int r = nsteps - (c + 2);  // steps issued but not needed by step c+1
+      if (g == 1) wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+    }
+    barrier_lds();
+    // ---- C(c)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (++cu_k == nks) cu_k = 0;
+    {
+      const int r = nsteps - (c + 2);
+      if (g == 0) wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+    }
+    barrier_lds();
+  }
+#undef GVL_PP3_ISSUE
+  if (g == 0) __builtin_amdgcn_s_barrier();
+  if (nsteps > 0) GVL_PP3_EPILOGUE();
+#undef GVL_PP3_EPILOGUE
+}
+
+template <int NS, bool AMN, bool BMN, int EPI>
+int launch_pp3(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;  // tiles_m/n, splits, kper set by gemm_pp3_try
+  constexpr int lds = NS * 512 * KS * 2;
+  auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  const int total = p.tiles_m * p.tiles_n * p.splits;
+  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, p);
+  if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
+  return 0;
+}
+
+template <int NS, bool AMN, bool BMN>
+int launch_pp3_epi(const GemmP& p, hipStream_t s) {
+  if (p.splits > 1) return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);  // partials only
+  switch (gvl::gemm_epi_kind(p)) {
+    case EPI_PLAIN: return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);
+    case EPI_BIAS: return launch_pp3<NS, AMN, BMN, EPI_BIAS>(p, s);
+    case EPI_BIAS_RES: return launch_pp3<NS, AMN, BMN, EPI_BIAS_RES>(p, s);
+    case EPI_BIAS_ACT: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT>(p, s);
+    case EPI_DACT: return launch_pp3<NS, AMN, BMN, EPI_DACT>(p, s);
+    default: return launch_pp2<4, 1, AMN, BMN>(p, s);
+  }
+}
+
+// cfg 0: NS=4, KC=1 (3 steps in flight, 32-MFMA clusters); 1: NS=4, KC=2 (64-MFMA clusters,
+// ring drained per cluster); 2: NS=5, KC=2 (one step in flight across the cluster barrier).
+template <bool AMN, bool BMN>
+int launch_layout(const GemmP& p, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 3: {
+      GemmP q = p;
+      if (gvl::gemm_pp3_plan(q, true)) return launch_pp3_epi<4, AMN, BMN>(q, s);
+      return launch_pp2<4, 1, AMN, BMN>(p, s);
+    }
+    case 1: return launch_pp2<4, 2, AMN, BMN>(p, s);
+    case 2: return launch_pp2<5, 2, AMN, BMN>(p, s);
+    default: return launch_pp2<4, 1, AMN, BMN>(p, s);
+  }
+}
+
+}  // namespace
+
+namespace gvl {
+const char* gemm_pp2_name(int cfg) {
+  switch (cfg) {
+    case 3: return "gemm_pp3_kernel<4";
+    case 1: return "gemm_pp2_kernel<4, 2";
+    case 2: return "gemm_pp2_kernel<5, 2";
+    default: return "gemm_pp2_kernel<4, 1";
+  }
+}
+
+int gemm_epi_kind(const GemmP& p) {
+  if (p.has_drop || p.gate || p.c_f32) return EPI_GEN;
+  const bool b = p.bias != nullptr, r = p.residual != nullptr;
+  if (!p.act && !p.dact) {
+    if (!b && !r) return EPI_PLAIN;
+    if (b && !r) return EPI_BIAS;
+    if (b && r) return EPI_BIAS_RES;
+    return EPI_GEN;
+  }
+  if (p.act && !p.dact && b && !r) return EPI_BIAS_ACT;
+  if (p.dact && !p.act && !b && !r) return EPI_DACT;
+  return EPI_GEN;
+}
+
+// Split-K factor for the persistent kernel: minimise the estimated time in units of one
+// 256x256 tile's 32-deep K-step, T(s) = rounds(tiles*s) * (K/32s + 6) + slab round trip
+// (s fp32 partials written + read, at ~6 TB/s, ~1.1 PF/s of MFMA per 256 CUs); slices must
+// be equal and at least 16 K-steps deep.
+int gemm_pp3_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int cus = num_cus();
+  const double step_s = 2.0 * 256 * 256 * 32 / (1.1e15 / cus);
+  double best = 1e30;
+  int best_s = 1;
+  for (int s = 1; s <= 16; ++s) {
+    if (K % (32 * s) != 0 || (s > 1 && K / s < 512)) continue;
+    const int64_t rounds = (tiles * s + cus - 1) / cus;
+    double t = (double)rounds * ((double)K / (32.0 * s) + 6.0);
+    if (s > 1) t += (double)s * M * N * 8.0 / 6e12 / step_s;
+    if (t < best * 0.97) { best = t; best_s = s; }
+  }
+  return best_s;
+}
+
+// Persistent-kernel plan: bf16 output with 16-B stores; tiles, split-K factor and K-slice
+// depth filled into p.  Without `force`, only when the work items fill the chip well enough
+// to beat the 128x128 ring (measured, tools/gemm_shapes.py): >= 160 items.
+bool gemm_pp3_plan(GemmP& p, bool force) {
+  if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
+  p.tiles_m = (int)((p.M + 255) / 256);
+  p.tiles_n = (int)((p.N + 255) / 256);
+  p.splits = 1;
+  if (p.ws != nullptr) {
+    const int sp = gemm_pp3_splits(p.M, p.N, p.K);
+    if (sp > 1 && (int64_t)sp * p.M * p.N * 4 <= p.ws_bytes) p.splits = sp;
+  }
+  p.kper = p.K / p.splits;
+  if (p.splits == 1 && gemm_epi_kind(p) == EPI_GEN) return false;
+  if (force) return true;
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+  // split-K slabs only pay off for really few tiles (dW, the caption lm_head dX); with
+  // >= 64 tiles the 128x128 ring at two workgroups per CU is faster
+  if (p.splits > 1 && tiles >= 64) return false;
+  return tiles * p.splits >= 160;
+}
+
+bool gemm_pp3_try(const GemmP& p0, int a_mn, int b_mn, hipStream_t s) {
+  GemmP p = p0;
+  if (!gemm_pp3_plan(p, false)) return false;
+  if (!a_mn && !b_mn) launch_pp3_epi<4, false, false>(p, s);
+  else if (!a_mn && b_mn) launch_pp3_epi<4, false, true>(p, s);
+  else if (a_mn && !b_mn) launch_pp3_epi<4, true, false>(p, s);
+  else launch_pp3_epi<4, true, true>(p, s);
+  return true;
+}
+
+int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s) {
+  if (!a_mn && !b_mn) return launch_layout<false, false>(p, cfg, s);
+  if (!a_mn && b_mn) return launch_layout<false, true>(p, cfg, s);
+  if (a_mn && !b_mn) return launch_layout<true, false>(p, cfg, s);
+  return launch_layout<true, true>(p, cfg, s);
+}
+}  // namespace gvl

@@ -191,9 +191,12 @@ __global__ __launch_bounds__(256) void ln_bwd_finalize(const float* __restrict__
   *dst = f2bf(t);
 }
 
+// Up to 1024 blocks (4 per CU resident beside the 32 KiB reduction array): at 512 the
+// 16k-row LM backward kept 8 waves per CU, each walking its rows one dependent load round
+// trip at a time (~2.3 TB/s); 1024 doubles the rows in flight.
 int ln_bwd_blocks(int64_t rows) {
   int64_t nb = (rows + 3) / 4;
-  if (nb > 512) nb = 512;
+  if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   return (int)nb;
 }

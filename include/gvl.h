@@ -76,9 +76,11 @@ typedef struct gvl_gemm_desc {
   const uint64_t* seed_ptr; /* optional device step offset re-keying `seed` (see below) */
 } gvl_gemm_desc;
 int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
-/* Process-wide GEMM implementation knob (benchmarking / A-B tests): impl 1 = LDS-DMA
- * kernel when K % 64 == 0 (default), 0 = register-staged kernel always; cfg -1 = pick
- * the tile by shape, 0/1/2 = force 256x256 / 256x128 / 128x128. */
+/* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):
+ * impl 3 (default) = persistent ping-pong 256x256 kernel (split-K for few tiles) where
+ * the work items fill the chip, else the 128x128 LDS-DMA ring; 2 = ring / non-persistent
+ * ping-pong family; 1 = LDS-DMA v2 (K % 64 == 0); 0 = register-staged kernel always.
+ * cfg -1 = pick by shape; otherwise forces a tile config of the family. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
  * caller attribute event timings to the rocprofv3 kernel-trace rows). */

@@ -56,9 +56,49 @@ def test_gemm_layouts(cuda, a_mn, b_mn, M, N, K):
     assert rel_err(c.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "bias_act", "dact", "generic"])
+@pytest.mark.parametrize("M,N,K", [(5000, 3080, 160), (4104, 2312, 32)])
+def test_gemm_persistent_epilogues(cuda, a_mn, b_mn, epi, M, N, K):
+    """Shapes with >= 160 tiles of 256x256 run the persistent ping-pong kernel (several tiles
+    per workgroup at 260 tiles, ragged M/N edges, 1- and 5-step tiles) with each
+    compile-time epilogue kind; 'generic' (dropout-free gate) takes the fallback path."""
+    K_ = _k()
+    torch.manual_seed(M + K + len(epi))
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.1).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    h = a.float() @ b.float()
+    kw, ref = {}, h
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    if epi == "bias":
+        kw, ref = dict(bias=bias.to(cuda)), h + bias.float()
+    elif epi == "bias_res":
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "bias_act":
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=1, pre_out=pre), O.gelu_tanh(h + bias.float())
+    elif epi == "dact":
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_erf(hx).sum().backward()
+        kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
+    elif epi == "generic":
+        gate = torch.tensor(0.3).to(BF)
+        kw = dict(residual=res.to(cuda), gate=gate.to(cuda))
+        ref = res.float() + math.tanh(float(gate.float())) * h
+    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    if epi == "bias_act":
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
                                              (0, 0, 384, 256, 6144)])
-def test_gemm_splitk_epilogue(cuda, a_mn, b_mn, M, N, K):
+@pytest.mark.parametrize("impl", [3, 2])
+def test_gemm_splitk_epilogue(cuda, a_mn, b_mn, M, N, K, impl):
     """Few output tiles + long K -> split-K partials + reduce kernel applying the epilogue."""
     K_ = _k()
     torch.manual_seed(M + K)
@@ -69,8 +109,13 @@ def test_gemm_splitk_epilogue(cuda, a_mn, b_mn, M, N, K):
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
     alpha = torch.tensor([0.5], dtype=torch.float32)
-    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), bias=bias.to(cuda), act=1,
-                residual=res.to(cuda), alpha_ptr=alpha.to(cuda))
+    from gvl import _lib
+    _lib.lib().gvl_gemm_tune(impl, -1)
+    try:
+        y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), bias=bias.to(cuda), act=1,
+                    residual=res.to(cuda), alpha_ptr=alpha.to(cuda))
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
     ref = O.gelu_tanh(0.5 * (a.float() @ b.float()) + bias.float()) + res.float()
     assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
 

@@ -1,6 +1,6 @@
 """Time every GEMM shape of the LM and Q-Former steps: libgvl (default pick and forced
 configs) next to torch.mm (hipBLASLt) as a yardstick.  One process, HIP events.
-python tools/gemm_shapes.py [lm|qf|all] [cfgs comma list, -1 = default pick]"""
+python tools/gemm_shapes.py [lm|qf|all] [impl:cfg comma list; 2:-1 = default pick]"""
 import os
 import sys
 
@@ -14,6 +14,7 @@ T = 16384  # LM tokens per micro-step
 Q = 8064   # Q-Former caption rows (128 x 63)
 QT = 3968  # caption text rows (128 x 31)
 # (name, M, N, K, a_mn, b_mn)
+BIG = [("big8k", 8192, 8192, 8192, 0, 0)]
 LM = [
     ("c_attn", T, 2304, 768, 0, 0), ("attn.c_proj", T, 768, 768, 0, 0),
     ("c_fc", T, 3072, 768, 0, 0), ("mlp.c_proj", T, 768, 3072, 0, 0),
@@ -37,8 +38,9 @@ QF = [
 
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1]
-    shapes = (LM if which in ("lm", "all") else []) + (QF if which in ("qf", "all") else [])
+    cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["2:-1"]
+    shapes = ((BIG if which in ("big", "all") else []) + (LM if which in ("lm", "all") else [])
+              + (QF if which in ("qf", "all") else []))
     L = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(0)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
@@ -52,18 +54,19 @@ def main():
         fl = 2.0 * M * N * Kd
         row = [f"{name:16s} {M:6d}x{N:6d}x{Kd:6d} {'tn'[am]}{'tn'[bm]}"]
         ref = None
-        for cfg in cfgs + [99]:
-            if cfg == 99:
+        for cfg in cfgs + ["torch"]:
+            if cfg == "torch":
                 at = A.t() if am else A
                 bt = B if bm else B.t()
                 fn = lambda: torch.mm(at, bt, out=C)  # noqa: E731
             else:
-                L.gvl_gemm_tune(2, cfg)
+                impl, c = (int(x) for x in cfg.split(":"))
+                L.gvl_gemm_tune(impl, c)
                 fn = lambda: K.gemm(A, B, a_mn=bool(am), b_mn=bool(bm), out=C)  # noqa: E731
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
-            if cfg == -1:
+            if ref is None:
                 ref = C.float().clone()
             elif ref is not None:
                 err = (C.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-9)
@@ -80,7 +83,7 @@ def main():
             tf = fl / us / 1e6
             tot.setdefault(cfg, 0.0)
             tot[cfg] += us
-            row.append(f"{'torch' if cfg == 99 else 'cfg' + str(cfg)}:{us:8.1f}us {tf:6.0f}TF")
+            row.append(f"{cfg}:{us:8.1f}us {tf:6.0f}TF")
         print(" ".join(row), flush=True)
         del A, B, C
     print("totals(us):", {k: round(v, 1) for k, v in tot.items()}, flush=True)
