@@ -14,6 +14,8 @@
 // dK/dV by a key-tile kernel (G groups of 16 keys per wave) looping over query tiles.
 // P is recomputed from the saved log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash
 // mask on (b,h,q,k), identical in every kernel.
+#include <algorithm>
+
 #include "common.h"
 #include "capi_util.h"
 #include "../../include/gvl.h"
@@ -47,6 +49,19 @@ struct AttnG {
   bf16_t* dv; int64_t dv_sb, dv_st, dv_sh;
   float* Dws;
 };
+
+// 1-D grid, heavy tiles first: the block id's slowest digit is the tile index, so every
+// (head, batch) pair's longest causal tile is dispatched in the first wave of blocks and the
+// short ones fill the tail.  LATE_HEAVY: the last query tiles see the most keys (forward,
+// dQ); otherwise the first key tiles see the most queries (dK/dV).
+template <bool LATE_HEAVY>
+GVL_DEV void tile_of_block(const AttnP& p, int64_t ntile, int64_t& t, int64_t& h, int64_t& b) {
+  const int64_t hb = p.H * p.B, bid = blockIdx.x;
+  const int64_t r = bid / hb, rem = bid - r * hb;
+  t = (LATE_HEAVY && p.causal) ? ntile - 1 - r : r;
+  b = rem / p.H;
+  h = rem - b * p.H;
+}
 
 // [64 rows][64 d] bf16 tile, 128-B rows.  Row image for ds_read_b128 fragments.
 GVL_DEV int swz_row(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -112,8 +127,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
-  const int64_t b = blockIdx.z, h = blockIdx.y;
-  const int64_t qblk0 = (int64_t)blockIdx.x * QT;
+  int64_t qt, h, b;
+  tile_of_block<true>(p, (p.Tq + QT - 1) / QT, qt, h, b);
+  const int64_t qblk0 = qt * QT;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
@@ -284,8 +300,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
-  const int64_t b = blockIdx.z, h = blockIdx.y;
-  const int64_t qblk0 = (int64_t)blockIdx.x * QT;
+  int64_t qt, h, b;
+  tile_of_block<true>(p, (p.Tq + QT - 1) / QT, qt, h, b);
+  const int64_t qblk0 = qt * QT;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
@@ -418,8 +435,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg)
   __shared__ __attribute__((aligned(16))) float sl[2][2][KT];         // [stage][lse2, D]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
-  const int64_t b = blockIdx.z, h = blockIdx.y;
-  const int64_t kblk0 = (int64_t)blockIdx.x * KB;
+  int64_t kt, h, b;
+  tile_of_block<false>(p, (p.Tk + KB - 1) / KB, kt, h, b);
+  const int64_t kblk0 = kt * KB;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
@@ -574,7 +592,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg)
 int fill(const gvl_attn_desc* d, AttnP& p) {
   GVL_REQUIRE(d && d->q && d->k && d->v && d->o, "gvl_attn: null tensor");
   GVL_REQUIRE(d->B > 0 && d->H > 0 && d->Tq > 0 && d->Tk > 0, "gvl_attn: empty shape");
-  GVL_REQUIRE(d->B <= 65535 && d->H <= 65535, "gvl_attn: B/H too large");
+  GVL_REQUIRE(d->B * d->H * ((std::max(d->Tq, d->Tk) + 63) / 64) < ((int64_t)1 << 31),
+              "gvl_attn: B*H*tiles too large for one grid");
   const int64_t st[] = {d->q_sb, d->q_st, d->q_sh, d->k_sb, d->k_st, d->k_sh,
                         d->v_sb, d->v_st, d->v_sh, d->o_sb, d->o_st, d->o_sh};
   for (int64_t s : st) GVL_REQUIRE(s % 8 == 0, "gvl_attn: strides must be multiples of 8 elements");
@@ -607,13 +626,16 @@ int fill(const gvl_attn_desc* d, AttnP& p) {
 // the short caption sequences (31-64 rows) keep 64-row blocks.
 int pick_groups(int64_t T) { return T > 64 ? 2 : 1; }
 
+// Block count of the 1-D heavy-first grid (see tile_of_block); fill() bounds it.
+unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntile * d->H * d->B); }
+
 }  // namespace
 
 extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   AttnP p;
   if (fill(d, p)) return -1;
   const int G = pick_groups(d->Tq);
-  dim3 grid((unsigned)((d->Tq + 64 * G - 1) / (64 * G)), (unsigned)d->H, (unsigned)d->B);
+  dim3 grid(grid_1d(d, (d->Tq + 64 * G - 1) / (64 * G)));
   hipStream_t s = gvl::as_stream(stream);
   if (G == 2) {
     if (p.has_drop) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(NT), 0, s, p);
@@ -654,7 +676,7 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
   const int Gq = pick_groups(d->Tq);
-  dim3 gq((unsigned)((d->Tq + 64 * Gq - 1) / (64 * Gq)), (unsigned)d->H, (unsigned)d->B);
+  dim3 gq(grid_1d(d, (d->Tq + 64 * Gq - 1) / (64 * Gq)));
   if (Gq == 2) {
     if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), gq, dim3(NT), 0, s, p, g);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), gq, dim3(NT), 0, s, p, g);
@@ -665,7 +687,7 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
   // dK/dV keeps one 16-key group per wave: two groups need >256 VGPRs (dK and dV
   // accumulators for 32 keys x 64 dims) and spill to scratch.
-  dim3 gk((unsigned)((d->Tk + 63) / 64), (unsigned)d->H, (unsigned)d->B);
+  dim3 gk(grid_1d(d, (d->Tk + 63) / 64));
   if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), gk, dim3(NT), 0, s, p, g);
   else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), gk, dim3(NT), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");

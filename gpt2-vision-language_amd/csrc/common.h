@@ -78,22 +78,37 @@ GVL_DEV float block_max(float v, float* red) {
 // GELU variants used by the reference: nn.GELU(approximate='tanh') in the GPT-2 MLP
 // (source/gpt2/train_gpt2.py:52) and exact-erf nn.GELU() in the Q-Former MLP
 // (source/gpt2_q_former/model.py:126-130).
+// These run in GEMM epilogues over every element of the MLP hidden layer, where the VALU
+// cost of libm tanhf/erff (~60 instructions) outweighed the tile's MFMA time; they are
+// written on bare v_exp_f32 / v_rcp_f32 instead:
+//   0.5 (1 + tanh(u)) = sigmoid(2u)   and   1 - tanh(u)^2 = 4 s (1 - s),
+// and erf by Abramowitz-Stegun 7.1.26 (|err| < 1.5e-7).  Both stay far inside the bf16
+// rounding of the stored values.
+GVL_DEV float fast_sigmoid(float z) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
 GVL_DEV float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return x * fast_sigmoid(2.f * k0 * (x + k1 * x * x * x));
 }
 GVL_DEV float dgelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float x2 = x * x;
+  const float s = fast_sigmoid(2.f * k0 * (x + k1 * x2 * x));
+  return s + 2.f * k0 * x * s * (1.f - s) * (1.f + 3.f * k1 * x2);
 }
-GVL_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+GVL_DEV float fast_erf(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * a);
+  const float poly =
+      t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float r = 1.f - poly * __builtin_amdgcn_exp2f(-1.4426950408889634f * a * a);
+  return copysignf(r, x);
+}
+GVL_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + fast_erf(x * 0.7071067811865476f)); }
 GVL_DEV float dgelu_erf(float x) {
-  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) +
-         x * 0.3989422804014327f * __expf(-0.5f * x * x);
+  return 0.5f * (1.f + fast_erf(x * 0.7071067811865476f)) +
+         x * 0.3989422804014327f * __builtin_amdgcn_exp2f(-0.7213475204444817f * x * x);
 }
 
 // Counter-based RNG for dropout masks (splitmix64 finaliser over (seed, index)).
