@@ -142,7 +142,10 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
 
 // Compile-time epilogue kinds for the persistent kernels (gemm_pp2.hip): each instance
 // carries only its own ops; EPI_GEN runs the runtime-flag path above.
-enum { EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5 };
+enum {
+  EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5,
+  EPI_RES = 6  // C = AB + residual (in-place gradient accumulation: residual == C)
+};
 
 template <int EPI>
 static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t a, int64_t m,
@@ -171,7 +174,7 @@ static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t 
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
     }
-    if constexpr (EPI == EPI_BIAS_RES) {
+    if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
       const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
       v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
     }

@@ -326,6 +326,7 @@ int launch_pp3_epi(const GemmP& p, hipStream_t s) {
     case EPI_BIAS_RES: return launch_pp3<NS, AMN, BMN, EPI_BIAS_RES>(p, s);
     case EPI_BIAS_ACT: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT>(p, s);
     case EPI_DACT: return launch_pp3<NS, AMN, BMN, EPI_DACT>(p, s);
+    case EPI_RES: return launch_pp3<NS, AMN, BMN, EPI_RES>(p, s);
     default: return launch_pp2<4, 1, AMN, BMN>(p, s);
   }
 }
@@ -365,7 +366,7 @@ int gemm_epi_kind(const GemmP& p) {
     if (!b && !r) return EPI_PLAIN;
     if (b && !r) return EPI_BIAS;
     if (b && r) return EPI_BIAS_RES;
-    return EPI_GEN;
+    return EPI_RES;
   }
   if (p.act && !p.dact && b && !r) return EPI_BIAS_ACT;
   if (p.dact && !p.act && !b && !r) return EPI_DACT;

@@ -6,7 +6,8 @@ Design (MI355X, one process per GPU, RCCL over xGMI via torch.distributed "nccl"
     bucket is a plain contiguous slice: no flatten/unflatten copies;
   * buckets are cut from the END of the arena (last layers first, matching the order in
     which backward produces gradients), ~bucket_mb each;
-  * a post-accumulate-grad hook marks parameters ready; on the sync micro-step the
+  * a post-accumulate-grad hook (or, for gradients the fused Functions accumulate in
+    place, gvl.functional's grad-ready hook) marks parameters ready; on the sync micro-step the
     bucket's all-reduce (AVG) is launched as soon as its last parameter is ready, so it
     overlaps the remaining backward on RCCL's own stream;
   * wait() joins every outstanding bucket into the current stream before clip + AdamW;
@@ -16,6 +17,8 @@ On a gloo group (CPU tests) AVG is emulated as SUM then divide, synchronously.
 from __future__ import annotations
 
 import torch.distributed as dist
+
+from . import functional as F
 
 
 def _is_nccl(pg):
@@ -53,6 +56,7 @@ class GradBuckets:
         self._handles = []
         self.sync = True
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p, _, _ in layout]
+        self._hooks.append(F.register_grad_ready_hook(self._on_fused))
 
     def _launch(self, bi):
         s, e, _ = self.buckets[bi]
@@ -68,6 +72,10 @@ class GradBuckets:
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
+
+    def _on_fused(self, p):
+        if p in self._bucket_of:
+            self._on_grad(p)
 
     def set_sync(self, flag: bool):
         """Enable the all-reduce for the coming backward (the last micro-step)."""

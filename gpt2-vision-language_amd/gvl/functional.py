@@ -39,6 +39,89 @@ def _need(ctx, i):
     return ctx.needs_input_grad[i]
 
 
+# ------------------------------------------------------- fused gradient accumulation
+# With gradient accumulation the reference lets autograd add every micro-step's weight
+# gradient into .grad (one extra read-modify-write pass per parameter per micro-step).
+# Here a parameter whose .grad already holds a bf16 buffer of its shape (the optimizer's
+# arena view after zero_grad, or the tensor autograd stored on the first micro-step) is a
+# "sink": the weight-gradient GEMM adds into it in its epilogue (C = dY^T X + C), bias and
+# LayerNorm gradients use their kernels' accumulate flag, and the Function returns None for
+# that input.  AccumulateGrad then never runs for it, so _ready() notifies the
+# data-parallel bucketing (gvl.dist) in its place.  Tied parameters (wte: embedding +
+# lm_head) keep the autograd path, which sums both uses before one AccumulateGrad.
+FUSE_GRAD_ACC = True
+_READY_HOOKS = []
+
+
+def register_grad_ready_hook(fn):
+    """fn(param) runs when a fused Function has finished accumulating param.grad."""
+    _READY_HOOKS.append(fn)
+
+    class _Handle:
+        @staticmethod
+        def remove():
+            if fn in _READY_HOOKS:
+                _READY_HOOKS.remove(fn)
+    return _Handle()
+
+
+def _sink(p):
+    if not FUSE_GRAD_ACC or not isinstance(p, torch.nn.Parameter):
+        return None
+    g = p.grad
+    if g is None or g.dtype != BF16 or g.shape != p.shape or not g.is_contiguous() or not g.is_cuda:
+        return None
+    return g
+
+
+def _ready(p):
+    for fn in _READY_HOOKS:
+        fn(p)
+
+
+def _wgrad(ctx, i, p, dy2, x2):
+    """nn.Linear weight gradient dy2^T x2 of input i (accumulated in place when p sinks)."""
+    if not _need(ctx, i):
+        return None
+    g = _sink(p)
+    if g is None:
+        return K.linear_dw(dy2, x2)
+    K.linear_dw(dy2, x2, out=g, residual=g)
+    _ready(p)
+    return None
+
+
+def _bgrad(ctx, i, p, dy2):
+    """Bias gradient (column sum of dy2) of input i."""
+    if not _need(ctx, i):
+        return None
+    g = _sink(p)
+    if g is None:
+        return K.colsum(dy2)
+    K.colsum(dy2, out=g, accumulate=True)
+    _ready(p)
+    return None
+
+
+def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx):
+    """LayerNorm backward writing/accumulating dx; returns the (dw, db) autograd outputs."""
+    nw, nb = _need(ctx, iw), _need(ctx, ib)
+    gw = _sink(w) if nw else None
+    gb = _sink(b) if nb else None
+    if (nw or nb) and (gw is not None or not nw) and (gb is not None or not nb):
+        K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=gw, db=gb,
+                        accumulate_wb=True)
+        for p, n in ((w, nw), (b, nb)):
+            if n:
+                _ready(p)
+        return None, None
+    C = x2.shape[1]
+    dw = torch.empty(C, dtype=BF16, device=x2.device) if nw else None
+    db = torch.empty(C, dtype=BF16, device=x2.device) if nb else None
+    K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=dw, db=db)
+    return dw, db
+
+
 # ------------------------------------------------------------------------ GPT-2 block
 class GPTBlockFn(torch.autograd.Function):
     """x + attn(ln_1 x); then + mlp(ln_2 .) — source/gpt2/train_gpt2.py:62-74.
@@ -69,6 +152,8 @@ class GPTBlockFn(torch.autograd.Function):
             ctx.save_for_backward(x2, xn1, m1, r1, qkv, y, lse, xm, xn2, m2, r2, hpre, h, ln1_w,
                                   attn_w, aproj_w, ln2_w, fc_w, mproj_w)
             ctx.shape = (B, T, C, n_head, causal)
+            ctx.params = (None, ln1_w, ln1_b, attn_w, attn_b, aproj_w, aproj_b, ln2_w, ln2_b,
+                          fc_w, fc_b, mproj_w, mproj_b)
         return out.view(B, T, C)
 
     @staticmethod
@@ -81,42 +166,29 @@ class GPTBlockFn(torch.autograd.Function):
         if d2.dtype != BF16:
             d2 = d2.to(BF16)
         d2 = d2.contiguous()
+        P = ctx.params
         # MLP c_proj
-        if _need(ctx, 11):
-            g[11] = K.linear_dw(d2, h)
-        if _need(ctx, 12):
-            g[12] = K.colsum(d2)
+        g[11] = _wgrad(ctx, 11, P[11], d2, h)
+        g[12] = _bgrad(ctx, 12, P[12], d2)
         dpre = K.linear_dx(d2, mproj_w, dact=1, pre_in=hpre)
-        if _need(ctx, 9):
-            g[9] = K.linear_dw(dpre, xn2)
-        if _need(ctx, 10):
-            g[10] = K.colsum(dpre)
+        g[9] = _wgrad(ctx, 9, P[9], dpre, xn2)
+        g[10] = _bgrad(ctx, 10, P[10], dpre)
         dxn2 = K.linear_dx(dpre, fc_w)
         dxm = d2.clone()
-        dw2 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 7) else None
-        db2 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 8) else None
-        K.layernorm_bwd(dxn2, xm, ln2_w, m2, r2, dx=dxm, accumulate_dx=True, dw=dw2, db=db2)
-        g[7], g[8] = dw2, db2
+        g[7], g[8] = _ln_bwd(ctx, 7, 8, P[7], P[8], dxn2, xm, m2, r2, dxm, True)
         # attention c_proj
-        if _need(ctx, 5):
-            g[5] = K.linear_dw(dxm, y.view(B * T, C))
-        if _need(ctx, 6):
-            g[6] = K.colsum(dxm)
+        g[5] = _wgrad(ctx, 5, P[5], dxm, y.view(B * T, C))
+        g[6] = _bgrad(ctx, 6, P[6], dxm)
         dy = K.linear_dx(dxm, aproj_w)
         dqkv = torch.empty(B * T, 3 * C, dtype=BF16, device=d2.device)
         q3 = qkv.view(B, T, 3 * C)
         dq3 = dqkv.view(B, T, 3 * C)
         K.attn_bwd(dy.view(B, T, C), q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], y, lse, H,
                    causal, dq3[:, :, :C], dq3[:, :, C:2 * C], dq3[:, :, 2 * C:])
-        if _need(ctx, 3):
-            g[3] = K.linear_dw(dqkv, xn1)
-        if _need(ctx, 4):
-            g[4] = K.colsum(dqkv)
+        g[3] = _wgrad(ctx, 3, P[3], dqkv, xn1)
+        g[4] = _bgrad(ctx, 4, P[4], dqkv)
         dxn1 = K.linear_dx(dqkv, attn_w)
-        dw1 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 1) else None
-        db1 = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 2) else None
-        K.layernorm_bwd(dxn1, x2, ln1_w, m1, r1, dx=dxm, accumulate_dx=True, dw=dw1, db=db1)
-        g[1], g[2] = dw1, db1
+        g[1], g[2] = _ln_bwd(ctx, 1, 2, P[1], P[2], dxn1, x2, m1, r1, dxm, True)
         g[0] = dxm.view(B, T, C) if _need(ctx, 0) else None
         return tuple(g)
 
@@ -134,6 +206,7 @@ class LayerNormFn(torch.autograd.Function):
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w, mean, rstd)
             ctx.shp = shp
+            ctx.params = (w, b)
         return y.view(shp)
 
     @staticmethod
@@ -141,12 +214,14 @@ class LayerNormFn(torch.autograd.Function):
         x2, w, mean, rstd = ctx.saved_tensors
         C = x2.shape[1]
         d2 = dy.reshape(-1, C).to(BF16).contiguous()
-        dw = torch.empty(C, dtype=BF16, device=x2.device) if _need(ctx, 1) else None
-        db = torch.empty(C, dtype=BF16, device=x2.device) if _need(ctx, 2) else None
-        dx = None
-        if _need(ctx, 0) or dw is not None or db is not None:
-            dx = K.layernorm_bwd(d2, x2, w, mean, rstd, dw=dw, db=db)
-        return (dx.view(ctx.shp) if (dx is not None and _need(ctx, 0)) else None), dw, db, None
+        dx = torch.empty(x2.shape[0], C, dtype=BF16, device=x2.device)
+        if _need(ctx, 1) or _need(ctx, 2):
+            dw, db = _ln_bwd(ctx, 1, 2, ctx.params[0], ctx.params[1], d2, x2, mean, rstd, dx,
+                             False)
+        else:
+            dw = db = None
+            K.layernorm_bwd(d2, x2, w, mean, rstd, dx=dx)
+        return (dx.view(ctx.shp) if _need(ctx, 0) else None), dw, db, None
 
 
 # ---------------------------------------------------------------------------- Linear
@@ -175,6 +250,7 @@ class LinearFn(torch.autograd.Function):
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w, gate, ybr)
             ctx.cfg = (shp, N, drop_p, seed, residual is not None)
+            ctx.params = (w, b)
         return y.view(*shp[:-1], N)
 
     @staticmethod
@@ -196,8 +272,8 @@ class LinearFn(torch.autograd.Function):
         if drop_p > 0:
             dbr = K.dropout_mask_apply(dbr, drop_p, seed, seed_ptr=_off(dbr, drop_p))
         dx = K.linear_dx(dbr, w).view(shp) if _need(ctx, 0) else None
-        dw = K.linear_dw(dbr, x2) if _need(ctx, 1) else None
-        db = K.colsum(dbr) if _need(ctx, 2) else None
+        dw = _wgrad(ctx, 1, ctx.params[0], dbr, x2)
+        db = _bgrad(ctx, 2, ctx.params[1], dbr)
         return dx, dw, db, dres, dgate, None, None
 
 
@@ -216,6 +292,7 @@ class MLPFn(torch.autograd.Function):
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, w1, w2, hpre, h)
             ctx.cfg = (shp, act, drop_p, seed, residual is not None)
+            ctx.params = (None, w1, b1, w2, b2)
         return y.view(*shp[:-1], w2.shape[0])
 
     @staticmethod
@@ -226,11 +303,12 @@ class MLPFn(torch.autograd.Function):
         dres = dy if (has_res and _need(ctx, 5)) else None
         if drop_p > 0:
             d2 = K.dropout_mask_apply(d2, drop_p, seed, seed_ptr=_off(d2, drop_p))
-        dw2 = K.linear_dw(d2, h) if _need(ctx, 3) else None
-        db2 = K.colsum(d2) if _need(ctx, 4) else None
+        P = ctx.params
+        dw2 = _wgrad(ctx, 3, P[3], d2, h)
+        db2 = _bgrad(ctx, 4, P[4], d2)
         dpre = K.linear_dx(d2, w2, dact=act, pre_in=hpre)
-        dw1 = K.linear_dw(dpre, x2) if _need(ctx, 1) else None
-        db1 = K.colsum(dpre) if _need(ctx, 2) else None
+        dw1 = _wgrad(ctx, 1, P[1], dpre, x2)
+        db1 = _bgrad(ctx, 2, P[2], dpre)
         dx = K.linear_dx(dpre, w1).view(shp) if _need(ctx, 0) else None
         return dx, dw1, db1, dw2, db2, dres, None, None, None
 
@@ -274,6 +352,7 @@ class MHAFn(torch.autograd.Function):
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse)
             ctx.cfg = (B, Tq, Tk, C, n_head, self_attn, p_attn, p_out, seed, sa)
+            ctx.params = (in_w, in_b, out_w, out_b)
         return out.view(B, Tq, C)
 
     @staticmethod
@@ -284,11 +363,27 @@ class MHAFn(torch.autograd.Function):
         dres = dout if _need(ctx, 6) else None
         dbr = (K.dropout_mask_apply(d2, p_out, seed, seed_ptr=_off(d2, p_out)) if p_out > 0
                else d2)
-        d_out_w = K.linear_dw(dbr, o.view(B * Tq, C)) if _need(ctx, 4) else None
-        d_out_b = K.colsum(dbr) if _need(ctx, 5) else None
+        P_in_w, P_in_b, P_out_w, P_out_b = ctx.params
+        d_out_w = _wgrad(ctx, 4, P_out_w, dbr, o.view(B * Tq, C))
+        d_out_b = _bgrad(ctx, 5, P_out_b, dbr)
         do = K.linear_dx(dbr, out_w).view(B, Tq, C)
-        din_w = torch.empty_like(in_w) if _need(ctx, 2) else None
-        din_b = torch.empty(3 * C, dtype=BF16, device=d2.device) if _need(ctx, 3) else None
+        # packed in_proj gradients: written into the sinks (accumulate) or fresh buffers
+        sw = _sink(P_in_w) if _need(ctx, 2) else None
+        sb = _sink(P_in_b) if _need(ctx, 3) else None
+        din_w = torch.empty_like(in_w) if (_need(ctx, 2) and sw is None) else None
+        din_b = (torch.empty(3 * C, dtype=BF16, device=d2.device)
+                 if (_need(ctx, 3) and sb is None) else None)
+        tw = sw if sw is not None else din_w
+        tb = sb if sb is not None else din_b
+
+        def wg(dy_, x_, rows):
+            if tw is not None:
+                K.linear_dw(dy_, x_, out=tw[rows], residual=tw[rows] if sw is not None else None)
+
+        def bg(dy_, rows):
+            if tb is not None:
+                K.colsum(dy_, out=tb[rows], accumulate=sb is not None)
+
         dq_in = dkv_in = None
         if self_attn:
             p3 = qkv.view(B, Tq, 3 * C)
@@ -297,10 +392,8 @@ class MHAFn(torch.autograd.Function):
             K.attn_bwd(do, p3[:, :, :C], p3[:, :, C:2 * C], p3[:, :, 2 * C:], o, lse, H, False,
                        dp3[:, :, :C], dp3[:, :, C:2 * C], dp3[:, :, 2 * C:], drop_p=p_attn,
                        seed=sa, seed_ptr=_off(do, p_attn))
-            if din_w is not None:
-                K.linear_dw(dqkv, q2, out=din_w)
-            if din_b is not None:
-                K.colsum(dqkv, out=din_b)
+            wg(dqkv, q2, slice(None))
+            bg(dqkv, slice(None))
             if _need(ctx, 0):
                 dq_in = K.linear_dx(dqkv, in_w).view(B, Tq, C)
         else:
@@ -312,16 +405,18 @@ class MHAFn(torch.autograd.Function):
             K.attn_bwd(do, q3, k3[:, :, :C], k3[:, :, C:], o, lse, H, False, dqp.view(B, Tq, C),
                        dk3[:, :, :C], dk3[:, :, C:], drop_p=p_attn, seed=sa,
                        seed_ptr=_off(do, p_attn))
-            if din_w is not None:
-                K.linear_dw(dqp, q2, out=din_w[:C])
-                K.linear_dw(dkvp, kv2, out=din_w[C:])
-            if din_b is not None:
-                K.colsum(dqp, out=din_b[:C])
-                K.colsum(dkvp, out=din_b[C:])
+            wg(dqp, q2, slice(0, C))
+            wg(dkvp, kv2, slice(C, None))
+            bg(dqp, slice(0, C))
+            bg(dkvp, slice(C, None))
             if _need(ctx, 0):
                 dq_in = K.linear_dx(dqp, in_w[:C]).view(B, Tq, C)
             if _need(ctx, 1):
                 dkv_in = K.linear_dx(dkvp, in_w[C:]).view(B, Tk, C)
+        if sw is not None:
+            _ready(P_in_w)
+        if sb is not None:
+            _ready(P_in_b)
         return dq_in, dkv_in, din_w, din_b, d_out_w, d_out_b, dres, None, None, None, None, None
 
 
@@ -346,6 +441,7 @@ class CrossAttnFn(torch.autograd.Function):
             ctx.save_for_backward(x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w,
                                   c_w, gate)
             ctx.cfg = (B, T, S, C, n_head)
+            ctx.params = (None, None, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b)
         return out.view(B, T, C)
 
     @staticmethod
@@ -359,10 +455,9 @@ class CrossAttnFn(torch.autograd.Function):
         dbr = K.gate_bwd(d2, ybr, gate, gacc)
         if _need(ctx, 10):
             g[10] = gacc.to(gate.dtype).view_as(gate)
-        if _need(ctx, 8):
-            g[8] = K.linear_dw(dbr, o.view(B * T, C))
-        if _need(ctx, 9):
-            g[9] = K.colsum(dbr)
+        P = ctx.params
+        g[8] = _wgrad(ctx, 8, P[8], dbr, o.view(B * T, C))
+        g[9] = _bgrad(ctx, 9, P[9], dbr)
         do = K.linear_dx(dbr, c_w).view(B, T, C)
         dqp = torch.empty(B * T, C, dtype=BF16, device=d2.device)
         dkvp = torch.empty(B * S, 2 * C, dtype=BF16, device=d2.device)
@@ -370,22 +465,15 @@ class CrossAttnFn(torch.autograd.Function):
         dk3 = dkvp.view(B, S, 2 * C)
         K.attn_bwd(do, qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], o, lse, H, False,
                    dqp.view(B, T, C), dk3[:, :, :C], dk3[:, :, C:])
-        if _need(ctx, 4):
-            g[4] = K.linear_dw(dqp, xn)
-        if _need(ctx, 5):
-            g[5] = K.colsum(dqp)
-        if _need(ctx, 6):
-            g[6] = K.linear_dw(dkvp, z2)
-        if _need(ctx, 7):
-            g[7] = K.colsum(dkvp)
+        g[4] = _wgrad(ctx, 4, P[4], dqp, xn)
+        g[5] = _bgrad(ctx, 5, P[5], dqp)
+        g[6] = _wgrad(ctx, 6, P[6], dkvp, z2)
+        g[7] = _bgrad(ctx, 7, P[7], dkvp)
         if _need(ctx, 1):
             g[1] = K.linear_dx(dkvp, kv_w).view(B, S, C)
         dxn = K.linear_dx(dqp, q_w)
         dx = d2.clone()
-        dw = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 2) else None
-        db = torch.empty(C, dtype=BF16, device=d2.device) if _need(ctx, 3) else None
-        K.layernorm_bwd(dxn, x2, ln_w, mean, rstd, dx=dx, accumulate_dx=True, dw=dw, db=db)
-        g[2], g[3] = dw, db
+        g[2], g[3] = _ln_bwd(ctx, 2, 3, P[2], P[3], dxn, x2, mean, rstd, dx, True)
         g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
         return tuple(g)
 

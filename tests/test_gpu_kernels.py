@@ -57,7 +57,8 @@ def test_gemm_layouts(cuda, a_mn, b_mn, M, N, K):
 
 
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "bias_act", "dact", "generic"])
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "res_inplace", "bias_act", "dact",
+                                 "generic"])
 @pytest.mark.parametrize("M,N,K", [(5000, 3080, 160), (4104, 2312, 32)])
 def test_gemm_persistent_epilogues(cuda, a_mn, b_mn, epi, M, N, K):
     """Shapes with >= 160 tiles of 256x256 run the persistent ping-pong kernel (several tiles
@@ -77,6 +78,9 @@ def test_gemm_persistent_epilogues(cuda, a_mn, b_mn, epi, M, N, K):
         kw, ref = dict(bias=bias.to(cuda)), h + bias.float()
     elif epi == "bias_res":
         kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "res_inplace":  # fused gradient accumulation: C += AB
+        acc = res.to(cuda)
+        kw, ref = dict(residual=acc, out=acc), h + res.float()
     elif epi == "bias_act":
         pre = torch.empty(M, N, dtype=BF, device=cuda)
         kw, ref = dict(bias=bias.to(cuda), act=1, pre_out=pre), O.gelu_tanh(h + bias.float())
@@ -118,6 +122,27 @@ def test_gemm_splitk_epilogue(cuda, a_mn, b_mn, M, N, K, impl):
         _lib.lib().gvl_gemm_tune(3, -1)
     ref = O.gelu_tanh(0.5 * (a.float() @ b.float()) + bias.float()) + res.float()
     assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 768, 16384), (2304, 768, 8192), (768, 3072, 4096)])
+@pytest.mark.parametrize("impl", [3, 2])
+def test_gemm_wgrad_inplace_accumulate(cuda, M, N, K, impl):
+    """Weight-gradient GEMM accumulating into the gradient it reads (C = dY^T X + C, the
+    fused gradient accumulation of gvl.functional), through split-K and whole-K tiles."""
+    K_ = _k()
+    torch.manual_seed(M + N + K)
+    dy = torch.randn(K, M).to(BF)
+    x = (torch.randn(K, N) * 0.05).to(BF)
+    g0 = torch.randn(M, N).to(BF)
+    from gvl import _lib
+    _lib.lib().gvl_gemm_tune(impl, -1)
+    try:
+        g = g0.to(cuda)
+        K_.linear_dw(dy.to(cuda), x.to(cuda), out=g, residual=g)
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+    ref = dy.float().t() @ x.float() + g0.float()
+    assert rel_err(g.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
 @pytest.mark.parametrize("act", [1, 2])

@@ -180,6 +180,31 @@ def test_grad_accumulation_equivalence(cuda, meta, golden):
     assert rel_err(grads[1].numpy(), grads[0].numpy()) < 2e-2
 
 
+@pytest.mark.parametrize("kind", ["gpt", "linear", "qformer", "cross"])
+def test_fused_grad_accumulation(cuda, golden, meta, kind):
+    """Gradients accumulated in place by the fused Functions (weight-gradient GEMM with the
+    grad as residual, accumulating bias / LayerNorm kernels) equal autograd's accumulation
+    over 3 micro-steps, and every grad stays a view of the optimizer's arena."""
+    import gvl.functional as F
+    from gvl.train import train_step
+    fx = golden(f"{kind}_tiny")
+    arenas = []
+    try:
+        for fused in (False, True):
+            F.FUSE_GRAD_ACC = fused
+            m = _model(kind, meta, cuda)
+            opt = m.configure_optimizers(weight_decay=0.1, learning_rate=0.0, device="cuda")
+            train_step(m, opt, [None] * 3, lambda mm, _b: _loss(kind, mm, fx, cuda)[1], 0.0)
+            ga = opt.grad_arena
+            for p, off, n in opt.arena_layout():
+                assert p.grad.data_ptr() == ga[off:off + n].data_ptr()
+            arenas.append(ga.float().cpu().clone())
+    finally:
+        F.FUSE_GRAD_ACC = True
+    assert arenas[1].abs().max() > 0
+    assert rel_err(arenas[1].numpy(), arenas[0].numpy()) < 1e-2
+
+
 def test_full_size_lm_loss(cuda, golden):
     """GPT-2 124M (vocab 50304), B=1, T=1024, recipe weights: loss vs the reference CPU path."""
     import gvl.gpt2 as g2
