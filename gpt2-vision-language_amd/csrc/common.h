@@ -25,6 +25,13 @@ GVL_DEV uint32_t pack2(float lo, float hi) {  // one v_cvt_pk_bf16_f32 (RNE)
 }
 GVL_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 GVL_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+GVL_DEV void unpack8(const uint4& u, float (&f)[8]) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+GVL_DEV uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
 
 // 16x16x32 bf16 MFMA: D = A(16x32) * B(32x16) + C.
 // Lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]; D[4(l>>4)+r][l&15].
@@ -87,15 +94,18 @@ GVL_DEV float block_max(float v, float* red) {
 GVL_DEV float fast_sigmoid(float z) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
 }
-GVL_DEV float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return x * fast_sigmoid(2.f * k0 * (x + k1 * x * x * x));
+// s = sigmoid(2u), u = k0 (x + k1 x^3), with 2 k0 log2(e) folded into the polynomial.
+GVL_DEV float gelu_tanh_sig(float x, float x2) {
+  constexpr float A = 2.f * 0.7978845608028654f * 1.4426950408889634f, B = A * 0.044715f;
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * fmaf(B, x2, A)));
 }
+GVL_DEV float gelu_tanh(float x) { return x * gelu_tanh_sig(x, x * x); }
 GVL_DEV float dgelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  // d/dx x s(2u) = s + 2 k0 x s (1 - s) (1 + 3 k1 x^2)
+  constexpr float C = 2.f * 0.7978845608028654f, D = 3.f * 0.044715f * C;
   const float x2 = x * x;
-  const float s = fast_sigmoid(2.f * k0 * (x + k1 * x2 * x));
-  return s + 2.f * k0 * x * s * (1.f - s) * (1.f + 3.f * k1 * x2);
+  const float s = gelu_tanh_sig(x, x2);
+  return fmaf(x * s * (1.f - s), fmaf(D, x2, C), s);
 }
 GVL_DEV float fast_erf(float x) {
   const float a = fabsf(x);

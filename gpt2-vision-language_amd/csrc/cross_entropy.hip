@@ -1,6 +1,8 @@
-// Fused softmax cross-entropy over bf16 logits (fp32 math): one 256-thread block per
-// target row, the whole row held in registers (<= 32 x 16-B chunks per thread, V <= 65536),
-// so logits are read from HBM once and dlogits = softmax - onehot written once.
+// Fused softmax cross-entropy over bf16 logits (fp32 math): one 512-thread block per
+// target row, the whole row held in registers (<= 16 x 16-B chunks per thread, V <= 65536),
+// so logits are read from HBM once and dlogits = softmax - onehot written once.  512 threads
+// keep the row buffer at 64 VGPRs, so 2+ rows per CU are resident and one row's reductions
+// overlap another's loads; exponentials are bare v_exp_f32 on log2e-prescaled inputs.
 // HBM-bound: 2*V (read) + 2*V (write) bytes per row.
 #include "common.h"
 #include "capi_util.h"
@@ -8,8 +10,9 @@
 
 namespace {
 
-constexpr int CE_NT = 256;
-constexpr int CE_MAXC = 32;
+constexpr int CE_NT = 512;
+constexpr int CE_MAXC = 16;
+constexpr float CE_L2E = 1.4426950408889634f;
 
 __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
     const bf16_t* __restrict__ logits, int64_t ldl, int64_t V, int64_t rpg, int64_t gstride,
@@ -45,6 +48,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
     }
   }
   mx = block_max<CE_NT>(mx, red);
+  const float mxl = mx * CE_L2E;
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < CE_MAXC; ++i) {
@@ -52,7 +56,9 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
     if (c < nch) {
       const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s += __expf(lo_bf(w[k]) - mx) + __expf(hi_bf(w[k]) - mx);
+      for (int k = 0; k < 4; ++k)
+        s += __builtin_amdgcn_exp2f(fmaf(lo_bf(w[k]), CE_L2E, -mxl)) +
+             __builtin_amdgcn_exp2f(fmaf(hi_bf(w[k]), CE_L2E, -mxl));
     }
   }
   s = block_sum<CE_NT>(s, red);
@@ -69,8 +75,8 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
         const int64_t base = (int64_t)c * 8;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float a = __expf(lo_bf(w[k]) - mx) * inv;
-          float b = __expf(hi_bf(w[k]) - mx) * inv;
+          float a = __builtin_amdgcn_exp2f(fmaf(lo_bf(w[k]), CE_L2E, -mxl)) * inv;
+          float b = __builtin_amdgcn_exp2f(fmaf(hi_bf(w[k]), CE_L2E, -mxl)) * inv;
           if (base + 2 * k == tgt) a -= 1.f;
           if (base + 2 * k + 1 == tgt) b -= 1.f;
           o[k] = pack2(a, b);

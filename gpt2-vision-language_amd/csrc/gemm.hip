@@ -218,7 +218,7 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg), tf[d->a_mn != 0],
                tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
-      const char* epi[7] = {"0", "1", "2", "3", "4", "5", "6"};
+      const char* epi[9] = {"0", "1", "2", "3", "4", "5", "6", "7", "8"};
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)]);
     } else {

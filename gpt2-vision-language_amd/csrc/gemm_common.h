@@ -108,16 +108,22 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
   if (p.dact) {
     const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
     const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+    if (p.dact == 1) {
+      for (int r = 0; r < 4; ++r) v[r] *= dgelu_tanh(h[r]);
+    } else {
+      for (int r = 0; r < 4; ++r) v[r] *= dgelu_erf(h[r]);
+    }
   }
   if (p.act) {
     if (p.pre_out) {
       *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
           make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
+    if (p.act == 1) {
+      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+    } else {
+      for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+    }
   }
   if (p.has_drop) {
     const uint64_t seed = seed_eff(p.seed, p.seed_ptr);
@@ -144,39 +150,89 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
 // carries only its own ops; EPI_GEN runs the runtime-flag path above.
 enum {
   EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5,
-  EPI_RES = 6  // C = AB + residual (in-place gradient accumulation: residual == C)
+  EPI_RES = 6,  // C = AB + residual (in-place gradient accumulation: residual == C)
+  EPI_BIAS_ACT_ERF = 7, EPI_DACT_ERF = 8  // 3 / 4 are the tanh-GELU forms
+};
+
+template <int EPI>
+struct EpiKind {
+  static constexpr bool ACT = EPI == EPI_BIAS_ACT || EPI == EPI_BIAS_ACT_ERF;
+  static constexpr bool DACT = EPI == EPI_DACT || EPI == EPI_DACT_ERF;
+  static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF;
+  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT;
+  static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES;
+  static constexpr bool AUX = DACT || RES;  // reads a bf16 [M, N] operand (pre_in / residual)
+};
+
+// Epilogue operands of the persistent kernel, fetched in batches: the bias at the tile's
+// first K-step (its wait then hides behind the whole tile), the [M, N] operand (pre_in /
+// residual, 64 VGPRs per tile: too many to hold across the MFMA cluster) in two half-tile
+// batches inside the epilogue, so the epilogue pays two memory latencies — not one per
+// fragment pair, each of which would also wait behind the LDS-DMA of later K-steps.
+// Lane (row l&15, column quad q) holds, per fragment (i, j), the 4 bf16 at row
+// mw0 + 16 i + (l & 15), cols nw0 + 16 j + 4 q.
+template <int FM, int FN, int EPI>
+struct EpiPre {
+  using KD = EpiKind<EPI>;
+  uint2 b[KD::BIAS ? FN : 1];
+  static constexpr int XH = FM / 2;  // the [M, N] operand is fetched half a tile at a time
+  uint2 x[KD::AUX ? XH : 1][KD::AUX ? FN : 1];
+  GVL_DEV void load_bias(const GemmP& p, int64_t nw0, int lane) {
+    if constexpr (KD::BIAS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = nw0 + 16 * j + 4 * (lane >> 4);
+        b[j] = n < p.N ? *reinterpret_cast<const uint2*>(p.bias + n) : make_uint2(0, 0);
+      }
+    }
+  }
+  // rows of fragments i0 .. i0 + XH - 1
+  GVL_DEV void load_aux(const GemmP& p, int64_t mw0, int64_t nw0, int lane, int i0) {
+    if constexpr (KD::AUX) {
+      const bf16_t* base = KD::DACT ? p.pre_in : p.residual;
+      const int64_t ld = KD::DACT ? p.ldp : p.ldr;
+#pragma unroll
+      for (int i = 0; i < XH; ++i) {
+        const int64_t m = mw0 + 16 * (i0 + i) + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int64_t n = nw0 + 16 * j + 4 * (lane >> 4);
+          x[i][j] = (m < p.M && n < p.N) ? *reinterpret_cast<const uint2*>(base + m * ld + n)
+                                         : make_uint2(0, 0);
+        }
+      }
+    }
+  }
 };
 
 template <int EPI>
 static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t a, int64_t m,
                                                           int64_t n, float alpha, float gatev,
-                                                          float (&v)[4]) {
+                                                          const uint2& bb, const uint2& ax,
+                                                          float (&v)[4], float (&pre)[4]) {
   if constexpr (EPI == EPI_GEN) {
     gemm_epi_vals(p, a, m, n, alpha, gatev, v);
   } else {
+    using KD = EpiKind<EPI>;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RES || EPI == EPI_BIAS_ACT) {
-      const uint2 bb = *reinterpret_cast<const uint2*>(p.bias + n);
+    if constexpr (KD::BIAS) {
       v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
     }
-    if constexpr (EPI == EPI_DACT) {
-      const uint2 hh = *reinterpret_cast<const uint2*>(p.pre_in + m * p.ldp + n);
-      const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
+    if constexpr (KD::DACT) {
+      const float h[4] = {lo_bf(ax.x), hi_bf(ax.x), lo_bf(ax.y), hi_bf(ax.y)};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] *= (p.dact == 1 ? dgelu_tanh(h[r]) : dgelu_erf(h[r]));
+      for (int r = 0; r < 4; ++r) v[r] *= KD::ERF ? dgelu_erf(h[r]) : dgelu_tanh(h[r]);
     }
-    if constexpr (EPI == EPI_BIAS_ACT) {
-      if (p.pre_out) {
-        *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    if constexpr (KD::ACT) {  // the caller stores the pre-activation (16-B stores)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pre[r] = v[r];
+        v[r] = KD::ERF ? gelu_erf(v[r]) : gelu_tanh(v[r]);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (p.act == 1 ? gelu_tanh(v[r]) : gelu_erf(v[r]));
     }
-    if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
-      const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + m * p.ldr + n);
-      v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+    if constexpr (KD::RES) {
+      v[0] += lo_bf(ax.x); v[1] += hi_bf(ax.x); v[2] += lo_bf(ax.y); v[3] += hi_bf(ax.y);
     }
   }
 }
@@ -201,7 +257,7 @@ static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a,
 // instruction writes 16 rows x 64 B instead of 16 rows x 32 B.
 template <int FM, int FN, int EPI = EPI_GEN>
 GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
-                             int64_t nw0, int lane, float alpha) {
+                             int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI>& pre) {
   static_assert(FN % 2 == 0, "fragment pairs");
   float gatev = 1.f;
   if constexpr (EPI == EPI_GEN) gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
@@ -213,6 +269,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
   for (int i = 0; i < FM; ++i) {
     const int64_t m = mw0 + i * 16 + (lane & 15);
     const bool mok = m < p.M;
+    if (EpiKind<EPI>::AUX && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i);
 #pragma unroll
     for (int j = 0; j < FN; j += 2) {
       const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
@@ -224,10 +281,26 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         y1 = pack2(acc[i][j + 1][2] * alpha, acc[i][j + 1][3] * alpha);
       } else {
         float v0[4] = {0.f, 0.f, 0.f, 0.f}, v1[4] = {0.f, 0.f, 0.f, 0.f};
-        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, v0);
-        if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, v1);
+        float h0[4] = {0.f, 0.f, 0.f, 0.f}, h1[4] = {0.f, 0.f, 0.f, 0.f};
+        using KD = EpiKind<EPI>;
+        const uint2 b0 = KD::BIAS ? pre.b[KD::BIAS ? j : 0] : make_uint2(0, 0);
+        const uint2 b1 = KD::BIAS ? pre.b[KD::BIAS ? j + 1 : 0] : make_uint2(0, 0);
+        constexpr int XH = EpiPre<FM, FN, EPI>::XH;
+        const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
+        const uint2 a1 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j + 1 : 0] : make_uint2(0, 0);
+        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0);
+        if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, b1, a1, v1, h1);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
         x1 = pack2(v1[0], v1[1]); y1 = pack2(v1[2], v1[3]);
+        if (KD::ACT && p.pre_out) {  // pre-activation: same lane swap, 16-B stores
+          const auto hx = __builtin_amdgcn_permlane16_swap(pack2(h0[0], h0[1]), pack2(h1[0], h1[1]),
+                                                           false, false);
+          const auto hy = __builtin_amdgcn_permlane16_swap(pack2(h0[2], h0[3]), pack2(h1[2], h1[3]),
+                                                           false, false);
+          const int64_t n = nw0 + 16 * (j + (q & 1)) + 8 * (q >> 1);
+          if (mok && n < p.N)
+            *reinterpret_cast<uint4*>(p.pre_out + m * p.ldp + n) = make_uint4(hx[0], hy[0], hx[1], hy[1]);
+        }
       }
       const auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
       const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);

@@ -249,12 +249,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   int64_t cu_m0, cu_n0, cu_k0;
   int cu_sp;
   tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp);
+  EpiPre<FM, FN, EPI> pre;
+  pre.load_bias(p, cu_n0 + bcol, lane);
 #define GVL_PP3_EPILOGUE()                                                                   \
   do {                                                                                       \
     if (p.splits > 1)                                                                        \
       gemm_store_partial<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane);           \
     else                                                                                     \
-      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha);         \
+      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre);    \
   } while (0)
 
   short8_t af[FM], bf[FN];
@@ -268,6 +270,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
         for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
       ++cu_t;
       tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp);
+      pre.load_bias(p, cu_n0 + bcol, lane);
     }
     const char* sl = smem + (c % NS) * SLOT;
 #pragma unroll
@@ -327,6 +330,8 @@ int launch_pp3_epi(const GemmP& p, hipStream_t s) {
     case EPI_BIAS_ACT: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT>(p, s);
     case EPI_DACT: return launch_pp3<NS, AMN, BMN, EPI_DACT>(p, s);
     case EPI_RES: return launch_pp3<NS, AMN, BMN, EPI_RES>(p, s);
+    case EPI_BIAS_ACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF>(p, s);
+    case EPI_DACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_DACT_ERF>(p, s);
     default: return launch_pp2<4, 1, AMN, BMN>(p, s);
   }
 }
@@ -368,8 +373,8 @@ int gemm_epi_kind(const GemmP& p) {
     if (b && r) return EPI_BIAS_RES;
     return EPI_RES;
   }
-  if (p.act && !p.dact && b && !r) return EPI_BIAS_ACT;
-  if (p.dact && !p.act && !b && !r) return EPI_DACT;
+  if (p.act && !p.dact && b && !r) return p.act == 1 ? EPI_BIAS_ACT : EPI_BIAS_ACT_ERF;
+  if (p.dact && !p.act && !b && !r) return p.dact == 1 ? EPI_DACT : EPI_DACT_ERF;
   return EPI_GEN;
 }
 
@@ -398,6 +403,7 @@ int gemm_pp3_splits(int64_t M, int64_t N, int64_t K) {
 // to beat the 128x128 ring (measured, tools/gemm_shapes.py): >= 160 items.
 bool gemm_pp3_plan(GemmP& p, bool force) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
+  if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
   p.tiles_m = (int)((p.M + 255) / 256);
   p.tiles_n = (int)((p.N + 255) / 256);
   p.splits = 1;

@@ -1,116 +1,150 @@
-// LayerNorm forward/backward (nn.LayerNorm, eps 1e-5 in the reference), one wave per row.
-// Row values stay in registers (C <= 1024, 4 bf16 per 8-byte load per lane), statistics
-// in fp32 (two-pass variance on the register copy), output bf16.
-// HBM-bound: fwd reads C*2 B and writes C*2 B (+8 B stats) per row.
+// LayerNorm forward/backward (nn.LayerNorm, eps 1e-5 in the reference), HBM-bound.
+// Forward layout: one HALF-wave (32 lanes) per row, 16-B accesses: lane l of the half holds
+// chunks l, l+32, l+64, ... of 8 columns (C = 768 -> 3 chunks, 24 values in registers), so a
+// load instruction moves 2 rows x 512 B.  Statistics in fp32 (two-pass variance on the
+// register copy), row reductions over the 32 lanes of the half.
+// Bytes per row: forward 2C read + 2C written (+8 B stats); backward reads x, dy (and dx when
+// accumulating) and writes dx: 4C..6C, plus the dw/db partials.
 #include "common.h"
 #include "capi_util.h"
 #include "../../include/gvl.h"
 
 namespace {
 
-constexpr int LN_NT = 256;       // 4 rows (waves) per block
-constexpr int LN_MAXIT = 4;      // 4 * 64 lanes * 4 elems = 1024 columns max
+constexpr int LN_FWD_NT = 256;   // 8 rows per block
+constexpr int LN_BWD_NT = 256;   // 4 waves, one row each (+1 prefetched)
+constexpr int LN_BWD_MAXB = 1024;
 
-__global__ __launch_bounds__(LN_NT) void ln_fwd_kernel(const bf16_t* __restrict__ x, int64_t ldx,
-                                                       const bf16_t* __restrict__ w,
-                                                       const bf16_t* __restrict__ b,
-                                                       bf16_t* __restrict__ y, int64_t ldy,
-                                                       float* __restrict__ mean_out,
-                                                       float* __restrict__ rstd_out, int64_t rows,
-                                                       int C, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (LN_NT / 64) + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const bf16_t* xr = x + row * ldx;
-  float v[LN_MAXIT][4];
+GVL_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int IT>
+__global__ __launch_bounds__(LN_FWD_NT) void ln_fwd_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                           const bf16_t* __restrict__ w,
+                                                           const bf16_t* __restrict__ b,
+                                                           bf16_t* __restrict__ y, int64_t ldy,
+                                                           float* __restrict__ mean_out,
+                                                           float* __restrict__ rstd_out,
+                                                           int64_t rows, int C, float eps) {
+  const int hl = threadIdx.x & 31;
+  const int64_t row = (int64_t)blockIdx.x * (LN_FWD_NT / 32) + (threadIdx.x >> 5);
+  const bool live = row < rows;  // (no early exit: the half-wave shuffles need both halves)
+  const bf16_t* xr = x + (live ? row : 0) * ldx;
+  float v[IT][8];
   float s = 0.f;
 #pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it) {
-    const int c = (lane + 64 * it) * 4;
-    if (c < C) {
-      const uint2 u = *reinterpret_cast<const uint2*>(xr + c);
-      v[it][0] = lo_bf(u.x); v[it][1] = hi_bf(u.x); v[it][2] = lo_bf(u.y); v[it][3] = hi_bf(u.y);
-      s += v[it][0] + v[it][1] + v[it][2] + v[it][3];
+  for (int it = 0; it < IT; ++it) {
+    const int c = (hl + 32 * it) * 8;
+    if (live && c < C) {
+      unpack8(*reinterpret_cast<const uint4*>(xr + c), v[it]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += v[it][r];
     } else {
-      v[it][0] = v[it][1] = v[it][2] = v[it][3] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[it][r] = 0.f;
     }
   }
-  const float mean = warp_sum(s) / (float)C;
+  const float mean = half_sum(s) / (float)C;
   float ss = 0.f;
 #pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it) {
-    const int c = (lane + 64 * it) * 4;
+  for (int it = 0; it < IT; ++it) {
+    const int c = (hl + 32 * it) * 8;
     if (c < C) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 8; ++r) {
         const float d = v[it][r] - mean;
         ss += d * d;
       }
     }
   }
-  const float var = warp_sum(ss) / (float)C;
-  const float rstd = rsqrtf(var + eps);
+  const float rstd = rsqrtf(half_sum(ss) / (float)C + eps);
+  if (!live) return;
   bf16_t* yr = y + row * ldy;
 #pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it) {
-    const int c = (lane + 64 * it) * 4;
+  for (int it = 0; it < IT; ++it) {
+    const int c = (hl + 32 * it) * 8;
     if (c < C) {
-      const uint2 wu = *reinterpret_cast<const uint2*>(w + c);
-      const uint2 bu = *reinterpret_cast<const uint2*>(b + c);
-      const float o0 = (v[it][0] - mean) * rstd * lo_bf(wu.x) + lo_bf(bu.x);
-      const float o1 = (v[it][1] - mean) * rstd * hi_bf(wu.x) + hi_bf(bu.x);
-      const float o2 = (v[it][2] - mean) * rstd * lo_bf(wu.y) + lo_bf(bu.y);
-      const float o3 = (v[it][3] - mean) * rstd * hi_bf(wu.y) + hi_bf(bu.y);
-      *reinterpret_cast<uint2*>(yr + c) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+      float wf[8], bf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
+      unpack8(*reinterpret_cast<const uint4*>(b + c), bf);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) o[r] = (v[it][r] - mean) * rstd * wf[r] + bf[r];
+      *reinterpret_cast<uint4*>(yr + c) = pack8(o);
     }
   }
-  if (lane == 0) {
+  if (hl == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
   }
 }
 
-// Backward. Each block walks rows blockIdx.x*4+wave, stepping gridDim.x*4; dw/db column
-// partials accumulate in registers and are reduced once per block into ws[block][2C].
-__global__ __launch_bounds__(LN_NT) void ln_bwd_kernel(
+// Backward: one wave per row (lane l holds 4-column chunks l, l+64, l+128: 8-B accesses keep
+// the per-lane state small — dw/db partials, w, the row in hand and the prefetched next row
+// fit ~100 VGPRs, 4 blocks per CU).  Wave w of block k walks rows k*4 + w, stepping
+// gridDim.x*4; the next row's x / dy / dx(prev) / stats loads are issued before the current
+// row is computed, so each wave keeps two rows of loads in flight.  dw/db column partials
+// accumulate in registers and are reduced once per block into ws[block][2C].
+template <int IT>
+__global__ __launch_bounds__(LN_BWD_NT) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dx, int64_t lddx, int acc_dx,
     float* __restrict__ ws, int64_t rows, int C) {
-  __shared__ float red[LN_NT / 64][1024 * 2];
+  __shared__ float red[LN_BWD_NT / 64][2 * 64 * 4 * IT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pw[LN_MAXIT][4], pb[LN_MAXIT][4];
+  float pw[IT][4], pb[IT][4];
+  uint2 wu[IT];
 #pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it)
+  for (int it = 0; it < IT; ++it) {
+    const int c = (lane + 64 * it) * 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) pw[it][r] = pb[it][r] = 0.f;
-  float wv[LN_MAXIT][4];
-#pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it) {
-    const int c = (lane + 64 * it) * 4;
-    if (c < C) {
-      const uint2 wu = *reinterpret_cast<const uint2*>(w + c);
-      wv[it][0] = lo_bf(wu.x); wv[it][1] = hi_bf(wu.x); wv[it][2] = lo_bf(wu.y); wv[it][3] = hi_bf(wu.y);
-    } else {
-      wv[it][0] = wv[it][1] = wv[it][2] = wv[it][3] = 0.f;
-    }
+    wu[it] = c < C ? *reinterpret_cast<const uint2*>(w + c) : make_uint2(0, 0);
   }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[LN_MAXIT][4], g[LN_MAXIT][4];
-    float s1 = 0.f, s2 = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * (LN_BWD_NT / 64);
+  int64_t row = (int64_t)blockIdx.x * (LN_BWD_NT / 64) + wave;
+  uint2 xu[IT], du[IT], pu[IT];
+  float mean = 0.f, rstd = 0.f;
+  auto fetch = [&](int64_t r) {
+    mean = mean_in[r];
+    rstd = rstd_in[r];
 #pragma unroll
-    for (int it = 0; it < LN_MAXIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int c = (lane + 64 * it) * 4;
       if (c < C) {
-        const uint2 xu = *reinterpret_cast<const uint2*>(x + row * ldx + c);
-        const uint2 du = *reinterpret_cast<const uint2*>(dy + row * lddy + c);
-        const float xs[4] = {lo_bf(xu.x), hi_bf(xu.x), lo_bf(xu.y), hi_bf(xu.y)};
-        const float ds[4] = {lo_bf(du.x), hi_bf(du.x), lo_bf(du.y), hi_bf(du.y)};
+        xu[it] = *reinterpret_cast<const uint2*>(x + r * ldx + c);
+        du[it] = *reinterpret_cast<const uint2*>(dy + r * lddy + c);
+        if (acc_dx) pu[it] = *reinterpret_cast<const uint2*>(dx + r * lddx + c);
+      }
+    }
+  };
+  if (row < rows) fetch(row);
+  for (; row < rows; row += stride) {
+    uint2 cx[IT], cd[IT], cp[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      cx[it] = xu[it];
+      cd[it] = du[it];
+      cp[it] = pu[it];
+    }
+    const float mu = mean, rs = rstd;
+    if (row + stride < rows) fetch(row + stride);
+    float xh[IT][4], g[IT][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int c = (lane + 64 * it) * 4;
+      if (c < C) {
+        const float xs[4] = {lo_bf(cx[it].x), hi_bf(cx[it].x), lo_bf(cx[it].y), hi_bf(cx[it].y)};
+        const float ds[4] = {lo_bf(cd[it].x), hi_bf(cd[it].x), lo_bf(cd[it].y), hi_bf(cd[it].y)};
+        const float ws4[4] = {lo_bf(wu[it].x), hi_bf(wu[it].x), lo_bf(wu[it].y), hi_bf(wu[it].y)};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          xh[it][r] = (xs[r] - mean) * rstd;
-          g[it][r] = ds[r] * wv[it][r];
+          xh[it][r] = (xs[r] - mu) * rs;
+          g[it][r] = ds[r] * ws4[r];
           s1 += g[it][r];
           s2 += g[it][r] * xh[it][r];
           pw[it][r] += ds[r] * xh[it][r];
@@ -123,82 +157,86 @@ __global__ __launch_bounds__(LN_NT) void ln_bwd_kernel(
     }
     const float m1 = warp_sum(s1) / (float)C, m2 = warp_sum(s2) / (float)C;
 #pragma unroll
-    for (int it = 0; it < LN_MAXIT; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int c = (lane + 64 * it) * 4;
       if (c < C) {
         float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = rstd * (g[it][r] - m1 - xh[it][r] * m2);
-        bf16_t* dst = dx + row * lddx + c;
+        for (int r = 0; r < 4; ++r) o[r] = rs * (g[it][r] - m1 - xh[it][r] * m2);
         if (acc_dx) {
-          const uint2 pu = *reinterpret_cast<const uint2*>(dst);
-          o[0] += lo_bf(pu.x); o[1] += hi_bf(pu.x); o[2] += lo_bf(pu.y); o[3] += hi_bf(pu.y);
+          o[0] += lo_bf(cp[it].x); o[1] += hi_bf(cp[it].x);
+          o[2] += lo_bf(cp[it].y); o[3] += hi_bf(cp[it].y);
         }
-        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        *reinterpret_cast<uint2*>(dx + row * lddx + c) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       }
     }
   }
   if (ws == nullptr) return;
+  constexpr int CM = 64 * 4 * IT;
 #pragma unroll
-  for (int it = 0; it < LN_MAXIT; ++it) {
+  for (int it = 0; it < IT; ++it) {
     const int c = (lane + 64 * it) * 4;
-    if (c < C) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        red[wave][c + r] = pw[it][r];
-        red[wave][1024 + c + r] = pb[it][r];
-      }
+    for (int r = 0; r < 4; ++r) {
+      red[wave][c + r] = pw[it][r];
+      red[wave][CM + c + r] = pb[it][r];
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += LN_NT) {
+  for (int c = threadIdx.x; c < C; c += LN_BWD_NT) {
     float a = 0.f, bsum = 0.f;
 #pragma unroll
-    for (int k = 0; k < LN_NT / 64; ++k) {
+    for (int k = 0; k < LN_BWD_NT / 64; ++k) {
       a += red[k][c];
-      bsum += red[k][1024 + c];
+      bsum += red[k][CM + c];
     }
     ws[(int64_t)blockIdx.x * 2 * C + c] = a;
     ws[(int64_t)blockIdx.x * 2 * C + C + c] = bsum;
   }
 }
 
-// Column reduction of the per-block partials: block = 64 columns x 4 partial-groups, each
-// thread summing nblk/4 partials with 8 independent loads in flight (the partials were
-// previously summed by one serial dependent-load chain per column: ~120 us).
-__global__ __launch_bounds__(256) void ln_bwd_finalize(const float* __restrict__ ws, int nblk,
-                                                       int C, bf16_t* __restrict__ dw,
-                                                       bf16_t* __restrict__ db, int acc) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+// Column reduction of the per-block partials: block = 16 columns x 64 partial groups; each
+// thread sums <= LN_BWD_MAXB/64 partials (all loads in flight), then the groups reduce in LDS.
+__global__ __launch_bounds__(1024) void ln_bwd_finalize(const float* __restrict__ ws, int nblk,
+                                                        int C, bf16_t* __restrict__ dw,
+                                                        bf16_t* __restrict__ db, int acc) {
+  __shared__ float red[64][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float s = 0.f;
   if (c < 2 * C) {
-    int k = g;
-    for (; k + 28 < nblk; k += 32) {
+    float v[LN_BWD_MAXB / 64];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += ws[(int64_t)(k + 4 * j) * 2 * C + c];
+    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) {
+      const int k = g + 64 * j;
+      v[j] = k < nblk ? ws[(int64_t)k * 2 * C + c] : 0.f;
     }
-    for (; k < nblk; k += 4) s[0] += ws[(int64_t)k * 2 * C + c];
+#pragma unroll
+    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) s += v[j];
   }
-  red[g][cl] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  red[g][cl] = s;
   __syncthreads();
-  if (g != 0 || c >= 2 * C) return;
-  float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (threadIdx.x >= 16 || c >= 2 * C) return;
+  float t = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) t += red[k][cl];
   bf16_t* dst = (c < C) ? (dw ? dw + c : nullptr) : (db ? db + (c - C) : nullptr);
   if (!dst) return;
   if (acc) t += bf2f(*dst);
   *dst = f2bf(t);
 }
 
-// Up to 1024 blocks (4 per CU resident beside the 32 KiB reduction array): at 512 the
-// 16k-row LM backward kept 8 waves per CU, each walking its rows one dependent load round
-// trip at a time (~2.3 TB/s); 1024 doubles the rows in flight.
+// >= 2 rows per wave, <= 1024 blocks (4 per CU: 16 waves, ~32 rows in flight per CU).
 int ln_bwd_blocks(int64_t rows) {
-  int64_t nb = (rows + 3) / 4;
-  if (nb > 1024) nb = 1024;
+  int64_t nb = (rows + 7) / 8;
+  if (nb > LN_BWD_MAXB) nb = LN_BWD_MAXB;
   if (nb < 1) nb = 1;
   return (int)nb;
+}
+
+bool ln_shape_ok(int64_t cols, int64_t ld1, int64_t ld2, const void* p1, const void* p2) {
+  return cols > 0 && cols <= 1024 && cols % 8 == 0 && ld1 % 8 == 0 && ld2 % 8 == 0 &&
+         gvl::aligned16(p1) && gvl::aligned16(p2);
 }
 
 }  // namespace
@@ -206,15 +244,22 @@ int ln_bwd_blocks(int64_t rows) {
 extern "C" int gvl_layernorm_fwd(const void* x, int64_t ldx, const void* w, const void* b, void* y,
                                  int64_t ldy, float* mean, float* rstd, int64_t rows, int64_t cols,
                                  float eps, gvl_stream_t stream) {
-  GVL_REQUIRE(cols > 0 && cols <= 1024 && cols % 4 == 0, "gvl_layernorm_fwd: cols=%lld unsupported",
-              (long long)cols);
-  GVL_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "gvl_layernorm_fwd: ld must be multiple of 4");
+  GVL_REQUIRE(ln_shape_ok(cols, ldx, ldy, x, y) && gvl::aligned16(w) && gvl::aligned16(b),
+              "gvl_layernorm_fwd: cols=%lld unsupported (need cols %% 8 == 0, <= 1024, ld %% 8 "
+              "== 0, 16-byte aligned rows)", (long long)cols);
   if (rows == 0) return 0;
-  const int grid = (int)((rows + 3) / 4);
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(grid), dim3(LN_NT), 0, gvl::as_stream(stream),
-                     static_cast<const bf16_t*>(x), ldx, static_cast<const bf16_t*>(w),
-                     static_cast<const bf16_t*>(b), static_cast<bf16_t*>(y), ldy, mean, rstd, rows,
-                     (int)cols, eps);
+  const int grid = (int)((rows + 7) / 8);
+  hipStream_t s = gvl::as_stream(stream);
+  const auto xp = static_cast<const bf16_t*>(x);
+  const auto wp = static_cast<const bf16_t*>(w);
+  const auto bp = static_cast<const bf16_t*>(b);
+  auto yp = static_cast<bf16_t*>(y);
+  if (cols <= 768)
+    hipLaunchKernelGGL(ln_fwd_kernel<3>, dim3(grid), dim3(LN_FWD_NT), 0, s, xp, ldx, wp, bp, yp,
+                       ldy, mean, rstd, rows, (int)cols, eps);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3(grid), dim3(LN_FWD_NT), 0, s, xp, ldx, wp, bp, yp,
+                       ldy, mean, rstd, rows, (int)cols, eps);
   GVL_LAUNCH_CHECK("gvl_layernorm_fwd");
   return 0;
 }
@@ -228,19 +273,29 @@ extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
                                  int64_t lddx, int32_t accumulate_dx, void* dw, void* db,
                                  int32_t accumulate_wb, void* workspace, int64_t rows, int64_t cols,
                                  gvl_stream_t stream) {
-  GVL_REQUIRE(cols > 0 && cols <= 1024 && cols % 4 == 0, "gvl_layernorm_bwd: cols unsupported");
+  GVL_REQUIRE(ln_shape_ok(cols, lddy, ldx, dy, x) && lddx % 8 == 0 && gvl::aligned16(dx) &&
+                  gvl::aligned16(w),
+              "gvl_layernorm_bwd: cols unsupported (need cols %% 8 == 0, <= 1024, ld %% 8 == 0, "
+              "16-byte aligned rows)");
   GVL_REQUIRE(!(dw || db) || workspace, "gvl_layernorm_bwd: dw/db need a workspace");
   if (rows == 0) return 0;
   const int nb = ln_bwd_blocks(rows);
   hipStream_t s = gvl::as_stream(stream);
   float* ws = (dw || db) ? static_cast<float*>(workspace) : nullptr;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(LN_NT), 0, s, static_cast<const bf16_t*>(dy),
-                     lddy, static_cast<const bf16_t*>(x), ldx, static_cast<const bf16_t*>(w), mean,
-                     rstd, static_cast<bf16_t*>(dx), lddx, (int)accumulate_dx, ws, rows, (int)cols);
+  const auto dyp = static_cast<const bf16_t*>(dy);
+  const auto xp = static_cast<const bf16_t*>(x);
+  const auto wp = static_cast<const bf16_t*>(w);
+  auto dxp = static_cast<bf16_t*>(dx);
+  if (cols <= 768)
+    hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(LN_BWD_NT), 0, s, dyp, lddy, xp, ldx, wp,
+                       mean, rstd, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(LN_BWD_NT), 0, s, dyp, lddy, xp, ldx, wp,
+                       mean, rstd, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd");
   if (ws) {
-    const int g2 = (int)((2 * cols + 63) / 64);
-    hipLaunchKernelGGL(ln_bwd_finalize, dim3(g2), dim3(256), 0, s, ws, nb, (int)cols,
+    const int g2 = (int)((2 * cols + 15) / 16);
+    hipLaunchKernelGGL(ln_bwd_finalize, dim3(g2), dim3(1024), 0, s, ws, nb, (int)cols,
                        static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), (int)accumulate_wb);
     GVL_LAUNCH_CHECK("gvl_layernorm_bwd(finalize)");
   }

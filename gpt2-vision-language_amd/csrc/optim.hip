@@ -20,14 +20,6 @@ int red_blocks(int64_t n8) {
   return (int)nb;
 }
 
-GVL_DEV void unpack8(const uint4& u, float (&f)[8]) {
-  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
-  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
-}
-GVL_DEV uint4 pack8(const float (&f)[8]) {
-  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
-}
-
 __global__ __launch_bounds__(RED_NT) void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n,
                                                        float* __restrict__ partial) {
   __shared__ float red[RED_NT / 64];
@@ -115,33 +107,37 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ p,
   }
 }
 
-// Column sums (bias gradients).  Block (cx, s): 64 column-threads x 8 columns (16-B loads,
-// one 1-KiB coalesced row segment per wave) x 4 row groups, over rows [s*chunk, (s+1)*chunk),
-// 4 rows in flight per thread; the 4 row groups reduce through LDS into ws[s][cols].
-constexpr int CS_SPLITS = 64;
+// Column sums (bias gradients), HBM-bound: 2 B read per element.  Block (cx, s): 16
+// column-threads x 8 columns (16-B loads, 256-B row segments) x 16 row groups over rows
+// [s*chunk, (s+1)*chunk), 8 independent loads in flight per thread; the row groups reduce
+// through LDS into ws[s][cols].  The split count is sized for >= ~768 blocks (the chip needs
+// ~64 KiB of loads in flight per CU) and stays <= 128 so the finishing kernel reads at most
+// 16 partials per thread, all in flight at once.
+constexpr int CS_COLS = 128;
+constexpr int CS_MAX_SPLITS = 128;
 
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ x,
                                                              int64_t rows, int64_t cols, int64_t ld,
                                                              int64_t chunk, float* __restrict__ ws) {
-  __shared__ float red[4][512];
-  const int ct = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 512 + ct * 8;
+  __shared__ float red[16][CS_COLS + 4];
+  const int ct = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int64_t c = (int64_t)blockIdx.x * CS_COLS + ct * 8;
   const int64_t r0 = (int64_t)blockIdx.y * chunk;
   const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < cols) {
     int64_t r = r0 + rg;
-    for (; r + 12 < r1; r += 16) {
-      uint4 u[4];
+    for (; r + 112 < r1; r += 128) {
+      uint4 u[8];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) u[k] = *reinterpret_cast<const uint4*>(x + (r + 4 * k) * ld + c);
+      for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const uint4*>(x + (r + 16 * k) * ld + c);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < 8; ++k) {
         s[0] += lo_bf(u[k].x); s[1] += hi_bf(u[k].x); s[2] += lo_bf(u[k].y); s[3] += hi_bf(u[k].y);
         s[4] += lo_bf(u[k].z); s[5] += hi_bf(u[k].z); s[6] += lo_bf(u[k].w); s[7] += hi_bf(u[k].w);
       }
     }
-    for (; r < r1; r += 4) {
+    for (; r < r1; r += 16) {
       const uint4 u = *reinterpret_cast<const uint4*>(x + r * ld + c);
       s[0] += lo_bf(u.x); s[1] += hi_bf(u.x); s[2] += lo_bf(u.y); s[3] += hi_bf(u.y);
       s[4] += lo_bf(u.z); s[5] += hi_bf(u.z); s[6] += lo_bf(u.w); s[7] += hi_bf(u.w);
@@ -150,31 +146,51 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __res
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[rg][ct * 8 + k] = s[k];
   __syncthreads();
-  for (int i = threadIdx.x; i < 512; i += 256) {
-    const int64_t cc = (int64_t)blockIdx.x * 512 + i;
-    if (cc < cols) ws[(int64_t)blockIdx.y * cols + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-  }
+  const int i = threadIdx.x & (CS_COLS - 1), half = threadIdx.x >> 7;
+  const int64_t cc = (int64_t)blockIdx.x * CS_COLS + i;
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t += red[8 * half + g][i];
+  __syncthreads();
+  if (half) red[0][i] = t;
+  __syncthreads();
+  if (!half && cc < cols) ws[(int64_t)blockIdx.y * cols + cc] = t + red[0][i];
 }
 
-__global__ void colsum_finish_kernel(const float* __restrict__ ws, int nb, int64_t cols,
-                                     bf16_t* __restrict__ out, int acc) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int k = 0;
-  for (; k + 8 <= nb; k += 8) {
+// Block: 32 columns x 8 partial groups; each thread sums <= 16 partials (independent loads).
+__global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restrict__ ws, int nb,
+                                                            int64_t cols, bf16_t* __restrict__ out,
+                                                            int acc) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t c = (int64_t)blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (c < cols) {
+    float v[CS_MAX_SPLITS / 8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += ws[(int64_t)(k + j) * cols + c];
+    for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) {
+      const int k = g + 8 * j;
+      v[j] = k < nb ? ws[(int64_t)k * cols + c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) s += v[j];
   }
-  for (; k < nb; ++k) s[0] += ws[(int64_t)k * cols + c];
-  float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  red[g][cl] = s;
+  __syncthreads();
+  if (g != 0 || c >= cols) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t += red[k][cl];
   if (acc) t += bf2f(out[c]);
   out[c] = f2bf(t);
 }
 
-int colsum_blocks(int64_t rows, int64_t* chunk) {
-  int64_t nb = (rows + 127) / 128;
-  if (nb > CS_SPLITS) nb = CS_SPLITS;
+int colsum_blocks(int64_t rows, int64_t cols, int64_t* chunk) {
+  const int64_t cb = (cols + CS_COLS - 1) / CS_COLS;
+  int64_t nb = (768 + cb - 1) / cb;
+  const int64_t by_rows = (rows + 63) / 64;  // >= 64 rows (4 per row group) per block
+  if (nb > by_rows) nb = by_rows;
+  if (nb > CS_MAX_SPLITS) nb = CS_MAX_SPLITS;
   if (nb < 1) nb = 1;
   *chunk = (rows + nb - 1) / nb;
   return (int)nb;
@@ -304,7 +320,7 @@ extern "C" int gvl_adamw_dev(void* p, const void* g, void* m, void* v, int64_t n
 
 extern "C" int64_t gvl_colsum_workspace_size(int64_t rows, int64_t cols) {
   int64_t chunk;
-  return (int64_t)colsum_blocks(rows, &chunk) * cols * (int64_t)sizeof(float);
+  return (int64_t)colsum_blocks(rows, cols, &chunk) * cols * (int64_t)sizeof(float);
 }
 
 extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
@@ -314,17 +330,18 @@ extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld,
   GVL_REQUIRE(rows == 0 || gvl::aligned16(x), "gvl_colsum: x must be 16-byte aligned");
   if (cols == 0) return 0;
   int64_t chunk;
-  const int nb = colsum_blocks(rows, &chunk);
+  const int nb = colsum_blocks(rows, cols, &chunk);
   hipStream_t s = gvl::as_stream(stream);
   if (rows == 0) {
     (void)hipMemsetAsync(workspace, 0, cols * sizeof(float), s);
   } else {
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols + 511) / 512), nb), dim3(256), 0, s,
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols + CS_COLS - 1) / CS_COLS), nb),
+                       dim3(256), 0, s,
                        static_cast<const bf16_t*>(x), rows, cols, ld, chunk,
                        static_cast<float*>(workspace));
     GVL_LAUNCH_CHECK("gvl_colsum(partial)");
   }
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((cols + 31) / 32)), dim3(256), 0, s,
                      static_cast<const float*>(workspace), rows == 0 ? 1 : nb, cols,
                      static_cast<bf16_t*>(out), (int)accumulate);
   GVL_LAUNCH_CHECK("gvl_colsum(finish)");

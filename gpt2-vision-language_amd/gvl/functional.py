@@ -540,6 +540,7 @@ class LMHeadLossFn(torch.autograd.Function):
         loss = out[0].clone()
         logits = logits.view(B, S, V)
         ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)  # no zero-filled [rows, V] grad for the logits
         if need:
             ctx.save_for_backward(x2, w, dl, out)
             ctx.cfg = (B, S, T, C, row_offset)
@@ -549,6 +550,8 @@ class LMHeadLossFn(torch.autograd.Function):
     def backward(ctx, _dlogits, dloss):
         x2, w, dl, out = ctx.saved_tensors
         B, S, T, C, off = ctx.cfg
+        if dloss is None:
+            return None, None, None, None, None, None
         scale = (dloss.float().reshape(1) * out[1:2]).contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:

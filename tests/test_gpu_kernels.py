@@ -203,7 +203,7 @@ def test_gemm_dropout_gate(cuda):
 
 
 # ------------------------------------------------------------------------- LayerNorm
-@pytest.mark.parametrize("rows,C", [(37, 128), (300, 768), (5, 1024)])
+@pytest.mark.parametrize("rows,C", [(37, 128), (300, 768), (5, 1024), (20011, 768), (1000, 520)])
 def test_layernorm_fwd_bwd(cuda, rows, C):
     K_ = _k()
     torch.manual_seed(rows)
@@ -227,6 +227,12 @@ def test_layernorm_fwd_bwd(cuda, rows, C):
     assert rel_err(dx.float().cpu().numpy(), (xr.grad + prev.float()).numpy()) < 1e-2
     assert rel_err(dw.float().cpu().numpy(), wr.grad.numpy()) < 1e-2
     assert rel_err(db.float().cpu().numpy(), br.grad.numpy()) < 1e-2
+    # accumulate_wb: dw/db += (fused gradient accumulation)
+    dw0, db0 = dw.float().cpu(), db.float().cpu()
+    K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd, dw=dw, db=db,
+                     accumulate_wb=True)
+    assert rel_err(dw.float().cpu().numpy(), (dw0 + wr.grad).numpy()) < 1e-2
+    assert rel_err(db.float().cpu().numpy(), (db0 + br.grad).numpy()) < 1e-2
 
 
 # ------------------------------------------------------------------------- attention
@@ -410,6 +416,24 @@ def test_grad_norm_and_adamw(cuda, golden):
     got = P.float().cpu()
     assert rel_err(got[:n1].numpy(), refp[0].reshape(-1).numpy()) < 1e-2
     assert rel_err(got[n1:].numpy(), refp[1].reshape(-1).numpy()) < 1e-2
+
+
+@pytest.mark.parametrize("rows,cols", [(16384, 768), (8064, 3072), (3, 2304), (0, 16), (777, 264)])
+def test_colsum_shapes(cuda, rows, cols):
+    """Bias-gradient column sums at the model's shapes (split partials + finish), plus the
+    accumulate flag used by fused gradient accumulation."""
+    K_ = _k()
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, cols).to(BF)
+    s = K_.colsum(x.to(cuda))
+    want = x.float().sum(0)
+    assert rel_err(s.float().cpu().numpy(), want.numpy()) < 8e-3 or rows == 0
+    if rows == 0:
+        assert s.float().abs().max().item() == 0
+    prev = torch.randn(cols).to(BF)
+    acc = prev.to(cuda)
+    K_.colsum(x.to(cuda), out=acc, accumulate=True)
+    assert rel_err(acc.float().cpu().numpy(), (want + prev.float()).numpy()) < 8e-3
 
 
 def test_colsum_dropout_gate(cuda):

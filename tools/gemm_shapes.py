@@ -36,8 +36,45 @@ QF = [
 ]
 
 
+def epilogues():
+    """Fused-epilogue cost at the LM step's shapes: each line times the plain GEMM and the
+    same GEMM with the epilogue the model uses (default kernel pick)."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    cases = [("c_fc+bias+gelu", T, 3072, 768, 0, "act"), ("mlp.c_proj.dX*dgelu", T, 3072, 768, 1, "dact"),
+             ("c_attn+bias", T, 2304, 768, 0, "bias"), ("mlp.c_proj+bias+res", T, 768, 3072, 0, "bias_res"),
+             ("c_fc.dW+=", 3072, 768, T, 2, "res"), ("q.c_fc+bias+gelu_erf", Q, 3072, 768, 0, "act_erf")]
+    for name, M, N, Kd, kind, epi in cases:
+        A = (torch.randn(Kd, M, device="cuda", generator=g) if kind == 2 else
+             torch.randn(M, Kd, device="cuda", generator=g)).bfloat16()
+        B = (torch.randn(Kd, N, device="cuda", generator=g) if kind else
+             torch.randn(N, Kd, device="cuda", generator=g)).bfloat16()
+        C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        aux = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+        bias = torch.randn(N, device="cuda", generator=g).bfloat16()
+        kw = {"act": dict(bias=bias, act=1, pre_out=aux), "act_erf": dict(bias=bias, act=2, pre_out=aux),
+              "dact": dict(dact=1, pre_in=aux), "bias": dict(bias=bias),
+              "bias_res": dict(bias=bias, residual=aux), "res": dict(residual=C)}[epi]
+        row = [f"{name:22s}"]
+        for label, extra in (("plain", {}), (epi, kw)):
+            fn = lambda: K.gemm(A, B, a_mn=kind == 2, b_mn=kind >= 1, out=C, **extra)  # noqa: E731
+            for _ in range(3):
+                fn()
+            e0, e1 = ev(), ev()
+            e0.record()
+            for _ in range(20):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            row.append(f"{label}:{e0.elapsed_time(e1) / 20 * 1e3:8.1f}us")
+        print(" ".join(row), flush=True)
+
+
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "epi":
+        _lib.load()
+        return epilogues()
     cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["2:-1"]
     shapes = ((BIG if which in ("big", "all") else []) + (LM if which in ("lm", "all") else [])
               + (QF if which in ("qf", "all") else []))
