@@ -42,8 +42,7 @@ def _need(ctx, i):
 # ------------------------------------------------------- fused gradient accumulation
 # With gradient accumulation the reference lets autograd add every micro-step's weight
 # gradient into .grad (one extra read-modify-write pass per parameter per micro-step).
-# Here a parameter whose .grad already holds a bf16 buffer of its shape (the optimizer's
-# arena view after zero_grad, or the tensor autograd stored on the first micro-step) is a
+# Here a parameter whose .grad is a view of a gvl.optim.AdamW arena (bf16, its shape) is a
 # "sink": the weight-gradient GEMM adds into it in its epilogue (C = dY^T X + C), bias and
 # LayerNorm gradients use their kernels' accumulate flag, and the Function returns None for
 # that input.  AccumulateGrad then never runs for it, so _ready() notifies the
@@ -66,7 +65,10 @@ def register_grad_ready_hook(fn):
 
 
 def _sink(p):
-    if not FUSE_GRAD_ACC or not isinstance(p, torch.nn.Parameter):
+    # only gradients that live in a gvl.optim.AdamW arena: their consumers (the fused
+    # optimizer, gvl.dist.GradBuckets) do not rely on AccumulateGrad hooks, which torch DDP
+    # and plain torch optimizers' users may
+    if not FUSE_GRAD_ACC or not getattr(p, "_gvl_grad_sink", False):
         return None
     g = p.grad
     if g is None or g.dtype != BF16 or g.shape != p.shape or not g.is_contiguous() or not g.is_cuda:

@@ -67,6 +67,7 @@ class AdamW(torch.optim.Optimizer):
             if p.grad is not None:
                 gview.copy_(p.grad)
             p.grad = gview
+            p._gvl_grad_sink = True  # gvl.functional may accumulate into this grad in place
             st = self.state[p]
             st["step"] = torch.zeros((), dtype=torch.float32)
             st["exp_avg"] = marena[o:o + n].view_as(p)

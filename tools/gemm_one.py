@@ -1,5 +1,5 @@
 """Run one GEMM shape with one kernel config repeatedly (for rocprofv3 PMC passes).
-python tools/gemm_one.py M N K a_mn b_mn impl cfg [iters]   (impl 3 = torch.mm)"""
+python tools/gemm_one.py M N K a_mn b_mn impl cfg [iters]   (impl 9 = torch.mm)"""
 import os
 import sys
 
@@ -18,7 +18,7 @@ A = (torch.randn(Kd, M, device="cuda", generator=g) if am else
 B = (torch.randn(Kd, N, device="cuda", generator=g) if bm else
      torch.randn(N, Kd, device="cuda", generator=g)).bfloat16()
 C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-if impl < 3:
+if impl < 9:
     L.gvl_gemm_tune(impl, cfg)
     fn = lambda: K.gemm(A, B, a_mn=bool(am), b_mn=bool(bm), out=C)  # noqa: E731
 else:
