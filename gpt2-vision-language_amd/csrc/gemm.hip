@@ -202,7 +202,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 5, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 6, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -222,11 +222,11 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)]);
     } else {
-      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1)),
+      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn)),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);
     }
   } else if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
-    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
+    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg, d->a_mn);
     snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(cfg), tf[d->a_mn != 0], tf[d->b_mn != 0]);
   } else if (env().impl >= 1 && gvl::gemm_lds_ok(d)) {
     const int cfg = gvl::gemm_lds_pick(d->m, d->n, d->k, env().cfg > 2 ? -1 : env().cfg);
@@ -265,13 +265,13 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
     if (env().cfg >= 0) {
       gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg, s);
     } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
-      gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1), s);
+      gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn), s);
     }
     GVL_LAUNCH_CHECK("gvl_gemm(pp)");
     return 0;
   }
   if (env().impl == 2 && gvl::gemm_ring_ok(d)) {
-    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg);
+    const int cfg = gvl::gemm_ring_pick(d->m, d->n, d->k, env().cfg, d->a_mn);
     gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, cfg, s);
     GVL_LAUNCH_CHECK("gvl_gemm(ring)");
     return 0;

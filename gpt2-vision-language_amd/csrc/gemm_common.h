@@ -339,7 +339,7 @@ void gemm_splitk_reduce_launch(const GemmP& p, hipStream_t s);
 const char* gemm_ring_name(int cfg);
 bool gemm_ring_ok(const gvl_gemm_desc* d);
 int gemm_ring_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
-int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced);
+int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced, int a_mn);
 const char* gemm_pp2_name(int cfg);
 int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
 int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels

@@ -309,10 +309,15 @@ int launch_cfg(const GemmP& p0, hipStream_t s) {
 
 // cfg: 0 = 256x256 (8 waves, P=2, 4 slots = 128 KiB), 1 = 256x128 (8 waves, 5 slots),
 //      2 = 128x128 (4 waves, 4 slots = 64 KiB, two workgroups per CU), 3 = 256x256, 5 slots,
-//      4 = 256x256 ping-pong, 4 slots, 5 = 256x256 ping-pong, 5 slots.
+//      4 = 256x256 ping-pong, 4 slots, 5 = 256x256 ping-pong, 5 slots,
+//      6 = 64x128 (2 waves of 64x64, 4 slots = 48 KiB, three workgroups per CU; needs a
+//          K-contiguous A: the MN-contiguous LDS image is 128 rows wide).
 template <bool AMN, bool BMN>
 int launch_layout(const GemmP& p, int cfg, hipStream_t s) {
   switch (cfg) {
+    case 6:
+      if constexpr (!AMN) return launch_cfg<64, 128, 1, 2, 4, 1, AMN, BMN>(p, s);
+      return launch_cfg<128, 128, 2, 2, 4, 1, AMN, BMN>(p, s);
     case 0: return launch_cfg<256, 256, 2, 4, 4, 2, AMN, BMN>(p, s);
     case 1: return launch_cfg<256, 128, 4, 2, 5, 1, AMN, BMN>(p, s);
     case 3: return launch_cfg<256, 256, 2, 4, 5, 2, AMN, BMN>(p, s);
@@ -332,6 +337,7 @@ const char* gemm_ring_name(int cfg) {
     case 3: return "gemm_ring_kernel<256, 256, 2, 4, 5, 2";
     case 4: return "gemm_pp_kernel<4";
     case 5: return "gemm_pp_kernel<5";
+    case 6: return "gemm_ring_kernel<64, 128, 1, 2, 4, 1";
     default: return "gemm_ring_kernel<128, 128, 2, 2, 4, 1";
   }
 }
@@ -355,10 +361,25 @@ namespace gvl {
 // Tile choice (measured, tools/gemm_sweep.sh on MI355X): the ping-pong 256x256 kernel once the
 // output has >= 192 of its tiles, except between 1 and 1.25 rounds of 256 CUs (a nearly empty
 // second round); else the 128x128 ring kernel at two workgroups per CU.
-int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced) {
+// GVL_RING_SMALL=<cfg> (1 = 256x128, 6 = 64x128) overrides that choice for outputs of
+// 256..512 tiles of 128x128 (A/B measurement; tools/gpu_ab.sh).  64x128 measured on the
+// Q-Former caption step (its N = 768 GEMMs at M = 8064): dominant GEMM 0.198 -> 0.200 of
+// peak but the step 13.0k -> 12.8k img/s, so it is not the default.
+static int ring_band_cfg() {
+  static const int cfg = [] {
+    const char* e = getenv("GVL_RING_SMALL");
+    return (e && (e[0] == '1' || e[0] == '6') && e[1] == 0) ? e[0] - '0' : 2;
+  }();
+  return cfg;
+}
+int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced, int a_mn) {
   if (forced >= 0) return forced;
   const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
-  if (t256 < 192 || (t256 > 256 && t256 <= 320)) return 2;
+  if (t256 < 192 || (t256 > 256 && t256 <= 320)) {
+    const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
+    if (!a_mn && t128 > 256 && t128 < 512) return ring_band_cfg();
+    return 2;
+  }
   return 4;
 }
 }  // namespace gvl

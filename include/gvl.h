@@ -80,7 +80,8 @@ int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
  * impl 3 (default) = persistent ping-pong 256x256 kernel (split-K for few tiles) where
  * the work items fill the chip, else the 128x128 LDS-DMA ring; 2 = ring / non-persistent
  * ping-pong family; 1 = LDS-DMA v2 (K % 64 == 0); 0 = register-staged kernel always.
- * cfg -1 = pick by shape; otherwise forces a tile config of the family. */
+ * cfg -1 = pick by shape; otherwise forces a tile config of the family (impl 2: 0 = 256x256,
+ * 1 = 256x128, 2 = 128x128, 3 = 256x256/5 slots, 4/5 = ping-pong, 6 = 64x128). */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
  * caller attribute event timings to the rocprofv3 kernel-trace rows). */

@@ -145,6 +145,42 @@ def test_gemm_wgrad_inplace_accumulate(cuda, M, N, K, impl):
     assert rel_err(g.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0)])
+@pytest.mark.parametrize("epi", ["bias_res", "bias_act", "dact"])
+@pytest.mark.parametrize("M,N,K", [(8064, 768, 768), (8064, 768, 3072), (5000, 904, 96)])
+@pytest.mark.parametrize("cfg", [-1, 6, 1])
+def test_gemm_ring_band(cuda, a_mn, b_mn, epi, M, N, K, cfg):
+    """Outputs of 256..512 tiles of 128x128 (the caption step's N = 768 GEMMs at M = 8064)
+    through the ring tile configs selectable for them: the default 128x128, 64x128 (K-contiguous
+    A only; an MN-contiguous A falls back to 128x128) and 256x128; ragged M/N edges and each
+    epilogue kind the caption step uses."""
+    K_ = _k()
+    from gvl import _lib
+    torch.manual_seed(M + N + K + len(epi))
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    h = a.float() @ b.float()
+    bias = torch.randn(N).to(BF)
+    if epi == "bias_res":
+        res = torch.randn(M, N).to(BF)
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "bias_act":
+        kw, ref = dict(bias=bias.to(cuda), act=2), O.gelu_erf(h + bias.float())
+    else:
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_tanh(hx).sum().backward()
+        kw, ref = dict(dact=1, pre_in=hpre.to(cuda)), h * hx.grad
+    _lib.lib().gvl_gemm_tune(2 if cfg >= 0 else 3, cfg)
+    try:
+        y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("act", [1, 2])
 def test_gemm_epilogue_act_bias_residual(cuda, act):
     K_ = _k()
