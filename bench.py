@@ -193,12 +193,28 @@ def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
     return dt, r
 
 
-def dominant_kernel(summary):
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC passes of the same bench
+    command (tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs,
+    FETCH_SIZE doubled per the gfx950 correction); None when not measured."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)["workloads"][{"lm": "lm", "qformer": "qf"}[workload]]
+        return t[kernel]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def dominant_kernel(summary, workload="lm"):
     name, s = max(summary.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = s["ms"] / s["launches"]
     achieved = s["flops"] / (s["ms"] * 1e-3) / 1e12
     return dict(kernel=name, bound="mfma", achieved=round(achieved, 1), peak=PEAK_BF16_TFLOPS,
-                unit="TFLOP/s", frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None,
+                unit="TFLOP/s", frac=round(achieved / PEAK_BF16_TFLOPS, 4),
+                traffic=pmc_traffic(workload, name), traffic_unit="bytes/launch",
                 launches=s["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 avg_flop_per_launch=s["flops"] / s["launches"],
                 all_gemm_frac=round(sum(v["flops"] for v in summary.values())
@@ -301,7 +317,7 @@ def main():
     timer = K.KernelTimer()
     dt, res = timed(step, args.steps, args.warmup, world, timer, graph=use_graph)
     value = units * args.steps / dt
-    roof = dominant_kernel(timer.summary())
+    roof = dominant_kernel(timer.summary(), args.workload)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -325,7 +341,7 @@ def main():
         out["caption_qformer"] = dict(
             value=round(cval, 1), unit="images/s", ms_per_step=round(cdt / args.caption_steps * 1e3, 3),
             step_mfma_frac=round(cval * CAP_FLOP_PER_IMAGE["qformer"] / 1e12 / PEAK_BF16_TFLOPS / world, 4),
-            loss=round(float(cres.loss), 5), config=ccfg, roofline=dominant_kernel(ctimer.summary()))
+            loss=round(float(cres.loss), 5), config=ccfg, roofline=dominant_kernel(ctimer.summary(), "qformer"))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload)
     if rank == 0:

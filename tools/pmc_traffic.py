@@ -1,0 +1,56 @@
+"""Per-kernel HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md § HBM):
+FETCH_SIZE counts half the bytes of wide coalesced streaming reads (every libgvl GEMM operand
+moves by 16-B-per-lane buffer_load ... lds), so it is doubled; WRITE_SIZE is exact for the
+16-B-per-lane stores the GEMM epilogues issue.
+usage: python tools/pmc_traffic.py DIR   (DIR holds {lm,qf}_{FETCH_SIZE,WRITE_SIZE}/**.csv)"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(gemm_\w+_kernel<[^>]*>|\(anonymous namespace\)::(\w+)|(\w+_kernel))", name)
+    if m and m.group(1).startswith("gemm_"):
+        return m.group(1)
+    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:120]
+
+
+def load(d, counter):
+    acc = defaultdict(lambda: [0.0, 0])
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] != counter:
+                    continue
+                k = short(row["Kernel_Name"])
+                acc[k][0] += float(row["Counter_Value"])
+                acc[k][1] += 1
+    return acc
+
+
+def main(root):
+    out = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                     "eager bench steps; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch",
+           "workloads": {}}
+    for wl in ("lm", "qf"):
+        fe = load(os.path.join(root, f"{wl}_FETCH_SIZE"), "FETCH_SIZE")
+        wr = load(os.path.join(root, f"{wl}_WRITE_SIZE"), "WRITE_SIZE")
+        ks = {}
+        for k in fe:
+            if k not in wr or not fe[k][1] or not wr[k][1]:
+                continue
+            f_kib, w_kib = fe[k][0] / fe[k][1], wr[k][0] / wr[k][1]
+            ks[k] = dict(launches=fe[k][1], fetch_kib=round(f_kib, 1), write_kib=round(w_kib, 1),
+                         hbm_bytes=round(2 * f_kib * 1024 + w_kib * 1024))
+        out["workloads"][wl] = dict(sorted(ks.items(), key=lambda kv: -kv[1]["hbm_bytes"] * kv[1]["launches"]))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic of the bench's kernels from PMC counters (MI355X_MICROARCH.md § HBM): one
+# rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), kernel-trace
+# only, eager step (graph replays are not attributed per dispatch), each pass time-limited.
+# Then tools/pmc_traffic.py turns them into per-launch bytes -> gpurun_out/pmc_traffic_$TAG.json.
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=${1:-x}
+OUT=gpurun_out/pmc_traffic_$TAG; mkdir -p $OUT
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/lm_$c -o run -- \
+    python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $OUT/lm_$c.log 2>&1 || exit $?
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/qf_$c -o run -- \
+    python bench.py --workload qformer --steps 2 --warmup 0 --no-cpu-baseline --no-graph > $OUT/qf_$c.log 2>&1 || exit $?
+done
+python tools/pmc_traffic.py $OUT > gpurun_out/pmc_traffic_$TAG.json
