@@ -15,10 +15,11 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(gemm_\w+_kernel<[^>]*>|\(anonymous namespace\)::(\w+)|(\w+_kernel))", name)
-    if m and m.group(1).startswith("gemm_"):
-        return m.group(1)
-    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:120]
+    """'void (anonymous namespace)::gemm_ring_kernel<128, ...>(GemmP)' -> 'gemm_ring_kernel<128, ...>'
+    (the names bench.py's kernel timer reports)."""
+    s = name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    m = re.match(r"[\w:]+<[^<>()]*>", s)
+    return m.group(0) if m else s.split("(")[0][:120]
 
 
 def load(d, counter):

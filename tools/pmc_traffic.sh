@@ -6,6 +6,9 @@
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=${1:-x}
 OUT=gpurun_out/pmc_traffic_$TAG; mkdir -p $OUT
+# a deep queue of eager dispatches under --pmc aborted once with HSA_STATUS_ERROR_INVALID_PACKET_FORMAT
+# (profiler packet injection); serialising dispatches keeps the queue shallow
+export AMD_SERIALIZE_KERNEL=3
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/lm_$c -o run -- \
     python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $OUT/lm_$c.log 2>&1 || exit $?
