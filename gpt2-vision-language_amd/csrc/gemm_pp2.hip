@@ -401,6 +401,16 @@ int gemm_pp3_splits(int64_t M, int64_t N, int64_t K) {
 // Persistent-kernel plan: bf16 output with 16-B stores; tiles, split-K factor and K-slice
 // depth filled into p.  Without `force`, only when the work items fill the chip well enough
 // to beat the 128x128 ring (measured, tools/gemm_shapes.py): >= 160 items.
+// Work-item floor for the persistent kernel (GVL_PP3_MIN overrides it for A/B measurement).
+static int64_t pp3_min_items() {
+  static const int64_t v = [] {
+    const char* e = getenv("GVL_PP3_MIN");
+    const long x = e ? atol(e) : 0;
+    return (int64_t)(x > 0 ? x : 160);
+  }();
+  return v;
+}
+
 bool gemm_pp3_plan(GemmP& p, bool force) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
@@ -418,7 +428,7 @@ bool gemm_pp3_plan(GemmP& p, bool force) {
   // split-K slabs only pay off for really few tiles (dW, the caption lm_head dX); with
   // >= 64 tiles the 128x128 ring at two workgroups per CU is faster
   if (p.splits > 1 && tiles >= 64) return false;
-  return tiles * p.splits >= 160;
+  return tiles * p.splits >= pp3_min_items();
 }
 
 bool gemm_pp3_try(const GemmP& p0, int a_mn, int b_mn, hipStream_t s) {
