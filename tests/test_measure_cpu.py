@@ -1,0 +1,51 @@
+"""Host-side measurement plumbing: PMC traffic table parsing and the bench's lookup of it."""
+import csv
+import importlib.util
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_kernel_name_shortening_matches_bench_names():
+    T = _load("pmc_traffic", os.path.join(ROOT, "tools", "pmc_traffic.py"))
+    assert T.short("void (anonymous namespace)::gemm_ring_kernel<128, 128, 2, 2, 4, 1, true, true>(GemmP)") \
+        == "gemm_ring_kernel<128, 128, 2, 2, 4, 1, true, true>"
+    assert T.short("(anonymous namespace)::ce_row_kernel(unsigned short const*, long)") == "ce_row_kernel"
+
+
+def test_traffic_table_from_counter_csvs(tmp_path):
+    T = _load("pmc_traffic", os.path.join(ROOT, "tools", "pmc_traffic.py"))
+    name = "void (anonymous namespace)::gemm_pp3_kernel<4, false, true, 0>(GemmP)"
+    for wl in ("lm", "qf"):
+        for ctr, vals in (("FETCH_SIZE", [100.0, 300.0]), ("WRITE_SIZE", [50.0, 50.0])):
+            d = tmp_path / f"{wl}_{ctr}" / "host"
+            d.mkdir(parents=True)
+            with open(d / "run_counter_collection.csv", "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+                w.writeheader()
+                for v in vals:
+                    w.writerow(dict(Kernel_Name=name, Counter_Name=ctr, Counter_Value=v))
+    import contextlib
+    import io
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        T.main(str(tmp_path))
+    out = json.loads(buf.getvalue())
+    k = out["workloads"]["lm"]["gemm_pp3_kernel<4, false, true, 0>"]
+    # FETCH_SIZE doubled (gfx950 streaming-read correction), both counters in KiB
+    assert k["launches"] == 2 and k["hbm_bytes"] == round(2 * 200.0 * 1024 + 50.0 * 1024)
+
+
+def test_committed_traffic_covers_bench_dominant_kernels():
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        t = json.load(f)["workloads"]
+    assert t["lm"]["gemm_ring_kernel<128, 128, 2, 2, 4, 1, true, true>"]["hbm_bytes"] > 0
+    assert t["qf"]["gemm_ring_kernel<128, 128, 2, 2, 4, 1, false, true>"]["hbm_bytes"] > 0
