@@ -1,5 +1,6 @@
 // Fused softmax cross-entropy over bf16 logits (fp32 math): one 512-thread block per
-// target row, the whole row held in registers (<= 16 x 16-B chunks per thread, V <= 65536),
+// target row (V need not be a multiple of 8: the row buffer is padded to a multiple of 8
+// columns and the tail columns count as -inf / get a zero gradient), the whole row held in registers (<= 16 x 16-B chunks per thread, V <= 65536),
 // so logits are read from HBM once and dlogits = softmax - onehot written once.  512 threads
 // keep the row buffer at 64 VGPRs, so 2+ rows per CU are resident and one row's reductions
 // overlap another's loads; exponentials are bare v_exp_f32 on log2e-prescaled inputs.
@@ -14,6 +15,18 @@ constexpr int CE_NT = 512;
 constexpr int CE_MAXC = 16;
 constexpr float CE_L2E = 1.4426950408889634f;
 
+// bf16 -inf in columns [nvalid, 8) of an 8-column chunk (exp2 of it is exactly 0, so the
+// softmax ignores them and their dlogits come out 0)
+GVL_DEV uint4 mask_tail(uint4 u, int64_t nvalid) {
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (2 * k >= nvalid) w[k] = (w[k] & 0xFFFF0000u) | 0xFF80u;
+    if (2 * k + 1 >= nvalid) w[k] = (w[k] & 0x0000FFFFu) | 0xFF800000u;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
     const bf16_t* __restrict__ logits, int64_t ldl, int64_t V, int64_t rpg, int64_t gstride,
     int64_t roff, const int64_t* __restrict__ targets, const uint8_t* __restrict__ mask,
@@ -26,7 +39,16 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
   bf16_t* dst = dlogits ? dlogits + r * ldd : nullptr;
   const int64_t tgt = targets[r];
   const bool valid = (tgt != -100) && (mask == nullptr || mask[r] != 0);
-  const int nch = (int)(V >> 3);
+  const int nch = (int)((V + 7) >> 3);
+  if (valid && (tgt < 0 || tgt >= V)) {
+    // out-of-range class index (torch raises; the host-side check in gvl.functional does
+    // too): never read outside the row, poison the loss instead
+    if (dst)
+      for (int c = tid; c < nch; c += CE_NT)
+        *reinterpret_cast<uint4*>(dst + (int64_t)c * 8) = make_uint4(0, 0, 0, 0);
+    if (tid == 0) row_loss[r] = __int_as_float(0x7fc00000);
+    return;
+  }
   if (!valid) {
     if (dst) {
       for (int c = tid; c < nch; c += CE_NT)
@@ -42,6 +64,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
     const int c = tid + i * CE_NT;
     if (c < nch) {
       buf[i] = *reinterpret_cast<const uint4*>(src + (int64_t)c * 8);
+      if ((int64_t)c * 8 + 8 > V) buf[i] = mask_tail(buf[i], V - (int64_t)c * 8);
       const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) mx = fmaxf(mx, fmaxf(lo_bf(w[k]), hi_bf(w[k])));
@@ -118,9 +141,13 @@ extern "C" int gvl_cross_entropy(const void* logits, int64_t ldl, int64_t rows, 
                                  const int64_t* targets, const uint8_t* mask, int32_t mask_mode,
                                  float* row_loss, void* dlogits, int64_t ldd, float* out,
                                  gvl_stream_t stream) {
-  GVL_REQUIRE(vocab % 8 == 0 && vocab / 8 <= (int64_t)CE_NT * CE_MAXC,
-              "gvl_cross_entropy: vocab=%lld must be a multiple of 8 and <= 65536", (long long)vocab);
-  GVL_REQUIRE(ldl % 8 == 0 && (!dlogits || ldd % 8 == 0), "gvl_cross_entropy: ld must be mult of 8");
+  const int64_t vpad = (vocab + 7) / 8 * 8;
+  GVL_REQUIRE(vocab > 0 && vpad / 8 <= (int64_t)CE_NT * CE_MAXC,
+              "gvl_cross_entropy: vocab=%lld unsupported (1..65536)", (long long)vocab);
+  GVL_REQUIRE(ldl % 8 == 0 && ldl >= vpad && (!dlogits || (ldd % 8 == 0 && ldd >= vpad)),
+              "gvl_cross_entropy: row strides must be multiples of 8 covering the vocab rounded "
+              "up to 8 (ldl=%lld ldd=%lld vocab=%lld)", (long long)ldl, (long long)ldd,
+              (long long)vocab);
   GVL_REQUIRE(rows_per_group > 0, "gvl_cross_entropy: rows_per_group must be > 0");
   GVL_REQUIRE(row_loss && out && targets, "gvl_cross_entropy: null buffer");
   hipStream_t s = gvl::as_stream(stream);

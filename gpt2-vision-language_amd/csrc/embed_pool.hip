@@ -11,13 +11,16 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
                                                       const bf16_t* __restrict__ wte,
                                                       const bf16_t* __restrict__ wpe,
                                                       bf16_t* __restrict__ out, int64_t n, int64_t T,
-                                                      int C, int64_t S, int64_t off) {
+                                                      int C, int64_t S, int64_t off, int64_t V) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
   const int lane = threadIdx.x & 63;
   const int64_t t = r % T;
   const int64_t orow = (r / T) * S + off + t;
-  const bf16_t* a = wte + idx[r] * (int64_t)C;
+  // an id outside [0, V) never reads outside wte: it embeds as row 0 (the host-side check
+  // in gvl.functional raises on it first, as nn.Embedding does)
+  const int64_t id = idx[r];
+  const bf16_t* a = wte + ((id >= 0 && id < V) ? id : 0) * (int64_t)C;
   const bf16_t* b = wpe + t * (int64_t)C;
   bf16_t* o = out + orow * (int64_t)C;
   for (int c = lane * 8; c < C; c += 512) {
@@ -36,14 +39,15 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int64_t* __restrict_
                                                       const bf16_t* __restrict__ dout,
                                                       float* __restrict__ dwte,
                                                       float* __restrict__ dwpe, int64_t n, int64_t T,
-                                                      int C, int64_t S, int64_t off) {
+                                                      int C, int64_t S, int64_t off, int64_t V) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
   const int lane = threadIdx.x & 63;
   const int64_t t = r % T;
   const int64_t orow = (r / T) * S + off + t;
   const bf16_t* g = dout + orow * (int64_t)C;
-  float* a = dwte ? dwte + idx[r] * (int64_t)C : nullptr;
+  const int64_t id = idx[r];
+  float* a = (dwte && id >= 0 && id < V) ? dwte + id * (int64_t)C : nullptr;
   float* b = dwpe ? dwpe + t * (int64_t)C : nullptr;
   for (int c = lane * 2; c < C; c += 128) {
     const uint32_t u = *reinterpret_cast<const uint32_t*>(g + c);
@@ -117,27 +121,29 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
 }  // namespace
 
 extern "C" int gvl_embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out,
-                                 int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
-                                 int64_t out_offset, gvl_stream_t stream) {
+                                 int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
+                                 int64_t out_rows_per_seq, int64_t out_offset,
+                                 gvl_stream_t stream) {
   GVL_REQUIRE(C % 8 == 0, "gvl_embedding_fwd: C must be a multiple of 8");
-  GVL_REQUIRE(T > 0, "gvl_embedding_fwd: T must be > 0");
+  GVL_REQUIRE(T > 0 && vocab > 0, "gvl_embedding_fwd: T and vocab must be > 0");
   if (n_tokens == 0) return 0;
   hipLaunchKernelGGL(emb_fwd_kernel, dim3((unsigned)((n_tokens + 3) / 4)), dim3(256), 0,
                      gvl::as_stream(stream), idx, static_cast<const bf16_t*>(wte),
                      static_cast<const bf16_t*>(wpe), static_cast<bf16_t*>(out), n_tokens, T, (int)C,
-                     out_rows_per_seq, out_offset);
+                     out_rows_per_seq, out_offset, vocab);
   GVL_LAUNCH_CHECK("gvl_embedding_fwd");
   return 0;
 }
 
 extern "C" int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc,
                                  float* dwpe_acc, int64_t n_tokens, int64_t T, int64_t C,
-                                 int64_t out_rows_per_seq, int64_t out_offset, gvl_stream_t stream) {
-  GVL_REQUIRE(C % 2 == 0 && T > 0, "gvl_embedding_bwd: bad shape");
+                                 int64_t vocab, int64_t out_rows_per_seq, int64_t out_offset,
+                                 gvl_stream_t stream) {
+  GVL_REQUIRE(C % 2 == 0 && T > 0 && vocab > 0, "gvl_embedding_bwd: bad shape");
   if (n_tokens == 0) return 0;
   hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)((n_tokens + 3) / 4)), dim3(256), 0,
                      gvl::as_stream(stream), idx, static_cast<const bf16_t*>(dout), dwte_acc,
-                     dwpe_acc, n_tokens, T, (int)C, out_rows_per_seq, out_offset);
+                     dwpe_acc, n_tokens, T, (int)C, out_rows_per_seq, out_offset, vocab);
   GVL_LAUNCH_CHECK("gvl_embedding_bwd");
   return 0;
 }

@@ -107,6 +107,61 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16_t* __restrict__ p,
   }
 }
 
+// Mixed-precision AdamW: fp32 master weights and moments, the bf16 compute copy the model
+// reads written alongside (28 B/param).  Keeps updates smaller than a bf16 ulp of the
+// weight (LayerNorm gains ~1.0 have ulp 2^-7 >> lr) instead of rounding them away, so the
+// trajectory follows the reference's fp32 CPU path (the parity oracle).
+__global__ __launch_bounds__(256) void adamw_master_kernel(
+    bf16_t* __restrict__ p, float* __restrict__ pm, const bf16_t* __restrict__ g,
+    float* __restrict__ m, float* __restrict__ v, int64_t n, int64_t n_decay, AdamP a,
+    const float* __restrict__ gscale, const float* __restrict__ hyper) {
+  const float cs = gscale ? *gscale : 1.f;
+  if (hyper) {
+    a.lr = hyper[0];
+    a.bc1 = 1.f - powf(a.b1, hyper[1]);
+    a.bc2_sqrt = sqrtf(1.f - powf(a.b2, hyper[1]));
+  }
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float fg[8], fp[8], fm[8], fv[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + i * 8), fg);
+    const float4* P4 = reinterpret_cast<const float4*>(pm + i * 8);
+    const float4* M4 = reinterpret_cast<const float4*>(m + i * 8);
+    const float4* V4 = reinterpret_cast<const float4*>(v + i * 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 a4 = P4[h], b4 = M4[h], c4 = V4[h];
+      fp[4 * h] = a4.x; fp[4 * h + 1] = a4.y; fp[4 * h + 2] = a4.z; fp[4 * h + 3] = a4.w;
+      fm[4 * h] = b4.x; fm[4 * h + 1] = b4.y; fm[4 * h + 2] = b4.z; fm[4 * h + 3] = b4.w;
+      fv[4 * h] = c4.x; fv[4 * h + 1] = c4.y; fv[4 * h + 2] = c4.z; fv[4 * h + 3] = c4.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gk = bf2f(f2bf(fg[k] * cs));
+      adam_elem(fp[k], gk, fm[k], fv[k], a, (i * 8 + k) < n_decay);
+    }
+    float4* Pw = reinterpret_cast<float4*>(pm + i * 8);
+    float4* Mw = reinterpret_cast<float4*>(m + i * 8);
+    float4* Vw = reinterpret_cast<float4*>(v + i * 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      Pw[h] = make_float4(fp[4 * h], fp[4 * h + 1], fp[4 * h + 2], fp[4 * h + 3]);
+      Mw[h] = make_float4(fm[4 * h], fm[4 * h + 1], fm[4 * h + 2], fm[4 * h + 3]);
+      Vw[h] = make_float4(fv[4 * h], fv[4 * h + 1], fv[4 * h + 2], fv[4 * h + 3]);
+    }
+    *reinterpret_cast<uint4*>(p + i * 8) = pack8(fp);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += 256) {
+      float fp = pm[i], fm = m[i], fv = v[i];
+      const float gk = bf2f(f2bf(bf2f(g[i]) * cs));
+      adam_elem(fp, gk, fm, fv, a, i < n_decay);
+      pm[i] = fp; m[i] = fm; v[i] = fv;
+      p[i] = f2bf(fp);
+    }
+  }
+}
+
 // Column sums (bias gradients), HBM-bound: 2 B read per element.  Block (cx, s): 16
 // column-threads x 8 columns (16-B loads, 256-B row segments) x 16 row groups over rows
 // [s*chunk, (s+1)*chunk), 8 independent loads in flight per thread; the row groups reduce
@@ -315,6 +370,25 @@ extern "C" int gvl_adamw_dev(void* p, const void* g, void* m, void* v, int64_t n
                      static_cast<bf16_t*>(m), static_cast<bf16_t*>(v), n, n_decay, a, grad_scale,
                      hyper);
   GVL_LAUNCH_CHECK("gvl_adamw_dev");
+  return 0;
+}
+
+extern "C" int gvl_adamw_master_dev(void* p, float* p_master, const void* g, float* m, float* v,
+                                    int64_t n, int64_t n_decay, const float* hyper, float beta1,
+                                    float beta2, float eps, float weight_decay,
+                                    const float* grad_scale, gvl_stream_t stream) {
+  GVL_REQUIRE(p && p_master && g && m && v && hyper, "gvl_adamw_master_dev: null buffer");
+  GVL_REQUIRE(gvl::aligned16(p) && gvl::aligned16(g) && gvl::aligned16(p_master) &&
+                  gvl::aligned16(m) && gvl::aligned16(v),
+              "gvl_adamw_master_dev: arenas must be 16-byte aligned");
+  if (n == 0) return 0;
+  AdamP a;
+  a.lr = 0.f; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.bc1 = 1.f; a.bc2_sqrt = 1.f;
+  hipLaunchKernelGGL(adamw_master_kernel, dim3(ew_blocks(n >> 3)), dim3(256), 0,
+                     gvl::as_stream(stream), static_cast<bf16_t*>(p), p_master,
+                     static_cast<const bf16_t*>(g), m, v, n, n_decay, a, grad_scale, hyper);
+  GVL_LAUNCH_CHECK("gvl_adamw_master_dev");
   return 0;
 }
 

@@ -12,6 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
+ABI_VERSION = 3  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -80,9 +81,9 @@ SIGNATURES = {
     "gvl_cross_entropy": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp,
                                     c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "gvl_embedding_fwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64,
-                                    c_vp]),
+                                    c_i64, c_vp]),
     "gvl_embedding_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64,
-                                    c_vp]),
+                                    c_i64, c_vp]),
     "gvl_pool_clip": (C.c_int, [c_vp, c_i32, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
     "gvl_grad_norm_workspace_size": (c_i64, [c_i64]),
     "gvl_grad_norm": (C.c_int, [c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
@@ -90,6 +91,8 @@ SIGNATURES = {
                             c_f32, c_i64, c_vp, c_vp]),
     "gvl_adamw_dev": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_f32, c_f32,
                                 c_f32, c_vp, c_vp]),
+    "gvl_adamw_master_dev": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32,
+                                       c_f32, c_f32, c_f32, c_vp, c_vp]),
     "gvl_colsum_workspace_size": (c_i64, [c_i64, c_i64]),
     "gvl_colsum": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,
@@ -124,6 +127,9 @@ def load(path: str | None = None):
             fn = getattr(lib, name)  # AttributeError -> missing export: fail loudly
             fn.restype = res
             fn.argtypes = args
+        if lib.gvl_abi_version() != ABI_VERSION:
+            raise ImportError(f"{p} has C-ABI v{lib.gvl_abi_version()}, the bindings expect "
+                              f"v{ABI_VERSION}: rebuild it (make -C gpt2-vision-language_amd/csrc)")
         if path is None:
             _lib = lib
         return lib

@@ -69,8 +69,8 @@ class GPT_previous(nn.Module):
         x = Fn.EmbedFn.apply(idx, bf(tr.wte.weight), bf(tr.wpe.weight), None)
         x = self.decode(x)
         if targets is None:
-            return Fn.LinearFn.apply(x, bf(self.lm_head.weight), None), None
-        return Fn.LMHeadLossFn.apply(x, bf(self.lm_head.weight), targets, 0, None, False)
+            return Fn.lm_logits(x, bf(self.lm_head.weight)), None
+        return Fn.lm_head_loss(x, bf(self.lm_head.weight), targets, 0, None, False)
 
 
 class Linear_Bridge(nn.Module):
@@ -172,7 +172,7 @@ class GPT_Caption(nn.Module):
 
     def _decode_transformer(self, full_embeds):
         x = self.gpt.decode(full_embeds)
-        return Fn.LinearFn.apply(x, bf(self.gpt.lm_head.weight), None)
+        return Fn.lm_logits(x, bf(self.gpt.lm_head.weight))
 
     def forward(self, patch_tokens, input_ids, labels=None):
         B, T_txt = input_ids.shape
@@ -192,8 +192,8 @@ class GPT_Caption(nn.Module):
         x = self.gpt.decode(full)
         w = bf(self.gpt.lm_head.weight)
         if labels is None:
-            return Fn.LinearFn.apply(x, w, None), None
-        return Fn.LMHeadLossFn.apply(x, w, labels, M, None, False)
+            return Fn.lm_logits(x, w), None
+        return Fn.lm_head_loss(x, w, labels, M, None, False)
 
     def configure_optimizers(self, weight_decay, learning_rate, device):
         return build_optimizer(self, weight_decay, learning_rate, device)

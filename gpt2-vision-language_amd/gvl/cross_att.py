@@ -128,10 +128,10 @@ class GPT(nn.Module):
         x = Fn.LayerNormFn.apply(x, bf(tr.ln_f.weight), bf(tr.ln_f.bias), 1e-5)
         w = bf(self.lm_head.weight)
         if targets is None:
-            return Fn.LinearFn.apply(x, w, None), None
+            return Fn.lm_logits(x, w), None
         if target_mask is None:
-            return Fn.LMHeadLossFn.apply(x, w, targets, 0, None, False)
-        return Fn.LMHeadLossFn.apply(x, w, targets, 0, target_mask.to(x.device), True)
+            return Fn.lm_head_loss(x, w, targets, 0, None, False)
+        return Fn.lm_head_loss(x, w, targets, 0, target_mask.to(x.device), True)
 
     def configure_optimizers(self, weight_decay, learning_rate, device):
         return build_optimizer(self, weight_decay, learning_rate, device)

@@ -9,6 +9,7 @@ weight-gradient GEMMs entirely via ctx.needs_input_grad.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -39,6 +40,37 @@ def _need(ctx, i):
     return ctx.needs_input_grad[i]
 
 
+# ------------------------------------------------------------------- index checks
+# nn.Embedding and F.cross_entropy raise on an id / class index outside the table
+# (train_gpt2.py:114-124).  The kernels never read outside their rows whatever the ids
+# (include/gvl.h ABI v3), and this host-side check raises like torch does.  It reads one
+# device scalar (a sync), so it is skipped inside a hipGraph capture (gvl.graph) and can be
+# turned off with GVL_CHECK_IDS=0.
+CHECK_IDS = os.environ.get("GVL_CHECK_IDS", "1") != "0"
+
+
+def check_index_range(t, n, what, ignore_index=None):
+    if not CHECK_IDS or t.numel() == 0 or (t.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return
+    bad = (t < 0) | (t >= n)
+    if ignore_index is not None:
+        bad &= t != ignore_index
+    if bool(bad.any()):
+        lo, hi = int(t.min()), int(t.max())
+        raise IndexError(f"gvl: {what} out of range [0, {n}) (min {lo}, max {hi})")
+
+
+def pad_vocab(w):
+    """(weight padded with zero rows to a multiple of 8, true vocab).  GPTConfig()'s default
+    vocab of 50257 (train_gpt2.py:79) is not a multiple of the GEMM's 8-column store; the
+    logits GEMM runs on the padded table and the CE kernel masks the pad columns.  The
+    reference trains with 50304, where this is the identity."""
+    V = w.shape[0]
+    if V % 8 == 0:
+        return w, V
+    return torch.cat([w, w.new_zeros((8 - V % 8, w.shape[1]))], 0), V
+
+
 # ------------------------------------------------------- fused gradient accumulation
 # With gradient accumulation the reference lets autograd add every micro-step's weight
 # gradient into .grad (one extra read-modify-write pass per parameter per micro-step).
@@ -64,11 +96,26 @@ def register_grad_ready_hook(fn):
     return _Handle()
 
 
-def _sink(p):
+def _ddp_forward_active():
+    """True while torch DDP runs its wrapped module's forward (DDP._inside_ddp_forward).
+    DDP's reducer all-reduces from AccumulateGrad hooks (train_gpt2.py:270,468), so a
+    Function built under it must hand its gradients to autograd instead of sinking them."""
+    ddp = torch.nn.parallel.DistributedDataParallel
+    return getattr(ddp, "_active_ddp_module", None) is not None
+
+
+def _mark(ctx):
+    """Forward-time decision whether this node may accumulate into arena grads in place."""
+    ctx.sink_ok = FUSE_GRAD_ACC and not _ddp_forward_active()
+
+
+def _sink(p, ctx=None):
     # only gradients that live in a gvl.optim.AdamW arena: their consumers (the fused
     # optimizer, gvl.dist.GradBuckets) do not rely on AccumulateGrad hooks, which torch DDP
     # and plain torch optimizers' users may
     if not FUSE_GRAD_ACC or not getattr(p, "_gvl_grad_sink", False):
+        return None
+    if ctx is not None and not getattr(ctx, "sink_ok", True):
         return None
     g = p.grad
     if g is None or g.dtype != BF16 or g.shape != p.shape or not g.is_contiguous() or not g.is_cuda:
@@ -85,7 +132,7 @@ def _wgrad(ctx, i, p, dy2, x2):
     """nn.Linear weight gradient dy2^T x2 of input i (accumulated in place when p sinks)."""
     if not _need(ctx, i):
         return None
-    g = _sink(p)
+    g = _sink(p, ctx)
     if g is None:
         return K.linear_dw(dy2, x2)
     K.linear_dw(dy2, x2, out=g, residual=g)
@@ -97,7 +144,7 @@ def _bgrad(ctx, i, p, dy2):
     """Bias gradient (column sum of dy2) of input i."""
     if not _need(ctx, i):
         return None
-    g = _sink(p)
+    g = _sink(p, ctx)
     if g is None:
         return K.colsum(dy2)
     K.colsum(dy2, out=g, accumulate=True)
@@ -108,8 +155,8 @@ def _bgrad(ctx, i, p, dy2):
 def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx):
     """LayerNorm backward writing/accumulating dx; returns the (dw, db) autograd outputs."""
     nw, nb = _need(ctx, iw), _need(ctx, ib)
-    gw = _sink(w) if nw else None
-    gb = _sink(b) if nb else None
+    gw = _sink(w, ctx) if nw else None
+    gb = _sink(b, ctx) if nb else None
     if (nw or nb) and (gw is not None or not nw) and (gb is not None or not nb):
         K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=gw, db=gb,
                         accumulate_wb=True)
@@ -156,6 +203,7 @@ class GPTBlockFn(torch.autograd.Function):
             ctx.shape = (B, T, C, n_head, causal)
             ctx.params = (None, ln1_w, ln1_b, attn_w, attn_b, aproj_w, aproj_b, ln2_w, ln2_b,
                           fc_w, fc_b, mproj_w, mproj_b)
+            _mark(ctx)
         return out.view(B, T, C)
 
     @staticmethod
@@ -209,6 +257,7 @@ class LayerNormFn(torch.autograd.Function):
             ctx.save_for_backward(x2, w, mean, rstd)
             ctx.shp = shp
             ctx.params = (w, b)
+            _mark(ctx)
         return y.view(shp)
 
     @staticmethod
@@ -253,6 +302,7 @@ class LinearFn(torch.autograd.Function):
             ctx.save_for_backward(x2, w, gate, ybr)
             ctx.cfg = (shp, N, drop_p, seed, residual is not None)
             ctx.params = (w, b)
+            _mark(ctx)
         return y.view(*shp[:-1], N)
 
     @staticmethod
@@ -295,6 +345,7 @@ class MLPFn(torch.autograd.Function):
             ctx.save_for_backward(x2, w1, w2, hpre, h)
             ctx.cfg = (shp, act, drop_p, seed, residual is not None)
             ctx.params = (None, w1, b1, w2, b2)
+            _mark(ctx)
         return y.view(*shp[:-1], w2.shape[0])
 
     @staticmethod
@@ -355,6 +406,7 @@ class MHAFn(torch.autograd.Function):
             ctx.save_for_backward(q2, kv2, in_w, out_w, qkv, qp, kvp, o, lse)
             ctx.cfg = (B, Tq, Tk, C, n_head, self_attn, p_attn, p_out, seed, sa)
             ctx.params = (in_w, in_b, out_w, out_b)
+            _mark(ctx)
         return out.view(B, Tq, C)
 
     @staticmethod
@@ -370,8 +422,8 @@ class MHAFn(torch.autograd.Function):
         d_out_b = _bgrad(ctx, 5, P_out_b, dbr)
         do = K.linear_dx(dbr, out_w).view(B, Tq, C)
         # packed in_proj gradients: written into the sinks (accumulate) or fresh buffers
-        sw = _sink(P_in_w) if _need(ctx, 2) else None
-        sb = _sink(P_in_b) if _need(ctx, 3) else None
+        sw = _sink(P_in_w, ctx) if _need(ctx, 2) else None
+        sb = _sink(P_in_b, ctx) if _need(ctx, 3) else None
         din_w = torch.empty_like(in_w) if (_need(ctx, 2) and sw is None) else None
         din_b = (torch.empty(3 * C, dtype=BF16, device=d2.device)
                  if (_need(ctx, 3) and sb is None) else None)
@@ -444,6 +496,7 @@ class CrossAttnFn(torch.autograd.Function):
                                   c_w, gate)
             ctx.cfg = (B, T, S, C, n_head)
             ctx.params = (None, None, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b)
+            _mark(ctx)
         return out.view(B, T, C)
 
     @staticmethod
@@ -489,6 +542,7 @@ class EmbedFn(torch.autograd.Function):
     def forward(ctx, idx, wte, wpe, prefix=None):
         B, T = idx.shape
         C = wte.shape[1]
+        check_index_range(idx, wte.shape[0], "token id")
         M = 0 if prefix is None else prefix.shape[1]
         S = M + T
         out = torch.empty(B, S, C, dtype=BF16, device=idx.device)
@@ -509,7 +563,7 @@ class EmbedFn(torch.autograd.Function):
         if _need(ctx, 1) or _need(ctx, 2):
             acc_te = torch.zeros(V, C, dtype=torch.float32, device=dout.device) if _need(ctx, 1) else None
             acc_pe = torch.zeros(P, C, dtype=torch.float32, device=dout.device) if _need(ctx, 2) else None
-            K.embedding_bwd(idx, dout, acc_te, acc_pe, T, S, M, C)
+            K.embedding_bwd(idx, dout, acc_te, acc_pe, T, S, M, C, V)
             if acc_te is not None:
                 dwte = acc_te.to(dt_te)
             if acc_pe is not None:
@@ -529,16 +583,19 @@ class LMHeadLossFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, w, targets, row_offset: int, mask=None, mask_mode: bool = False):
+    def forward(ctx, x, w, targets, row_offset: int, mask=None, mask_mode: bool = False,
+                vocab: int = None):
         B, S, C = x.shape
         T = targets.shape[1]
         x2 = x.reshape(B * S, C).to(BF16).contiguous()
         logits = K.linear(x2, w)
         V = w.shape[0]
+        vocab = V if vocab is None else vocab
+        check_index_range(targets, vocab, "target", ignore_index=-100)
         need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         out, dl = K.cross_entropy(logits, targets, rows_per_group=T, group_stride=S,
                                   row_offset=row_offset, mask=mask, mask_mode=mask_mode,
-                                  want_grad=need)
+                                  want_grad=need, vocab=vocab)
         loss = out[0].clone()
         logits = logits.view(B, S, V)
         ctx.mark_non_differentiable(logits)
@@ -553,7 +610,7 @@ class LMHeadLossFn(torch.autograd.Function):
         x2, w, dl, out = ctx.saved_tensors
         B, S, T, C, off = ctx.cfg
         if dloss is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         scale = (dloss.float().reshape(1) * out[1:2]).contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -569,7 +626,23 @@ class LMHeadLossFn(torch.autograd.Function):
             else:
                 xt = x2.view(B, S, C)[:, off:off + T].reshape(B * T, C).contiguous()
             dw = K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
+
+
+def lm_head_loss(x, w, targets, row_offset=0, mask=None, mask_mode=False):
+    """(logits, loss) of the tied lm_head + CE for any vocab size (pads V to 8 if needed)."""
+    wp, V = pad_vocab(w)
+    logits, loss = LMHeadLossFn.apply(x, wp, targets, row_offset, mask, mask_mode, V)
+    if wp is not w:
+        logits = logits[..., :V].contiguous()
+    return logits, loss
+
+
+def lm_logits(x, w):
+    """logits = x w^T for the lm_head (any vocab size)."""
+    wp, V = pad_vocab(w)
+    logits = LinearFn.apply(x, wp, None)
+    return logits if wp is w else logits[..., :V].contiguous()
 
 
 def pool_clip(tokens):

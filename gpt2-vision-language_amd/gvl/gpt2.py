@@ -180,9 +180,9 @@ class GPT(nn.Module):
             x = blk(x)
         x = Fn.LayerNormFn.apply(x, bf(tr.ln_f.weight), bf(tr.ln_f.bias), 1e-5)
         if targets is None:
-            logits = Fn.LinearFn.apply(x, bf(self.lm_head.weight), None)
+            logits = Fn.lm_logits(x, bf(self.lm_head.weight))
             return logits, None
-        return Fn.LMHeadLossFn.apply(x, bf(self.lm_head.weight), targets, 0, None, False)
+        return Fn.lm_head_loss(x, bf(self.lm_head.weight), targets, 0, None, False)
 
     def configure_optimizers(self, weight_decay, learning_rate, device):
         return build_optimizer(self, weight_decay, learning_rate, device)

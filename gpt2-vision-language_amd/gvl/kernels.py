@@ -269,10 +269,12 @@ def attn_bwd(dout, q, k, v, o, lse, H, causal, dq, dk, dv, scale=None, drop_p=0.
 
 # ---------------------------------------------------------------------- cross entropy
 def cross_entropy(logits2, targets, *, rows_per_group=None, group_stride=0, row_offset=0,
-                  mask=None, mask_mode=False, want_grad=True):
-    """Returns (loss_and_inv [2] fp32 device tensor, dlogits [rows, V] bf16 or None)."""
+                  mask=None, mask_mode=False, want_grad=True, vocab=None):
+    """Returns (loss_and_inv [2] fp32 device tensor, dlogits [rows, V] bf16 or None).
+    `vocab` < logits2.shape[1] marks the trailing columns as padding (V % 8 != 0)."""
     _dev(logits2, targets)
-    V = logits2.shape[1]
+    Vp = logits2.shape[1]
+    V = Vp if vocab is None else int(vocab)
     rows = targets.numel()
     if rows_per_group is None:
         rows_per_group = max(rows, 1)
@@ -284,7 +286,7 @@ def cross_entropy(logits2, targets, *, rows_per_group=None, group_stride=0, row_
     if mask is not None:
         mk = mask.reshape(-1).to(torch.uint8).contiguous()
     row_loss = torch.empty(max(rows, 1), dtype=F32, device=logits2.device)
-    dl = torch.empty(rows, V, dtype=BF16, device=logits2.device) if want_grad else None
+    dl = torch.empty(rows, Vp, dtype=BF16, device=logits2.device) if want_grad else None
     out = torch.empty(2, dtype=F32, device=logits2.device)
     _lib.check(_L().gvl_cross_entropy(logits2.data_ptr(), logits2.stride(0), rows, V,
                                       rows_per_group, group_stride, row_offset, tg.data_ptr(),
@@ -298,17 +300,17 @@ def cross_entropy(logits2, targets, *, rows_per_group=None, group_stride=0, row_
 def embedding_fwd(idx, wte, wpe, out, T, out_rows_per_seq, out_offset):
     _dev(idx, wte, wpe, out)
     idx = idx.contiguous()
-    C_ = wte.shape[1]
+    V, C_ = wte.shape
     _lib.check(_L().gvl_embedding_fwd(idx.data_ptr(), wte.data_ptr(), wpe.data_ptr(),
-                                      out.data_ptr(), idx.numel(), T, C_, out_rows_per_seq,
+                                      out.data_ptr(), idx.numel(), T, C_, V, out_rows_per_seq,
                                       out_offset, _stream()), "gvl_embedding_fwd")
     return out
 
 
-def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset, C_):
+def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset, C_, V):
     idx = idx.contiguous()
     _lib.check(_L().gvl_embedding_bwd(idx.data_ptr(), dout.data_ptr(), _p(dwte_acc),
-                                      _p(dwpe_acc), idx.numel(), T, C_, out_rows_per_seq,
+                                      _p(dwpe_acc), idx.numel(), T, C_, V, out_rows_per_seq,
                                       out_offset, _stream()), "gvl_embedding_bwd")
 
 
@@ -347,6 +349,19 @@ def adamw_dev(p, g, m, v, n_decay, hyper, beta1, beta2, eps, wd, grad_scale=None
                                   p.numel(), int(n_decay), hyper.data_ptr(), float(beta1),
                                   float(beta2), float(eps), float(wd), _p(grad_scale), _stream()),
                "gvl_adamw_dev")
+
+
+def adamw_master_dev(p, p_master, g, m, v, n_decay, hyper, beta1, beta2, eps, wd,
+                     grad_scale=None):
+    """Mixed-precision AdamW: fp32 master / moments, bf16 compute copy p (gvl.h)."""
+    _dev(p, p_master, g, m, v, hyper)
+    if p_master.dtype != F32 or m.dtype != F32 or v.dtype != F32:
+        raise TypeError("gvl.adamw_master_dev: master / moments must be fp32")
+    _lib.check(_L().gvl_adamw_master_dev(p.data_ptr(), p_master.data_ptr(), g.data_ptr(),
+                                         m.data_ptr(), v.data_ptr(), p.numel(), int(n_decay),
+                                         hyper.data_ptr(), float(beta1), float(beta2), float(eps),
+                                         float(wd), _p(grad_scale), _stream()),
+               "gvl_adamw_master_dev")
 
 
 def adamw(p, g, m, v, n_decay, lr, beta1, beta2, eps, wd, step, grad_scale=None):

@@ -18,6 +18,7 @@ import torch
 from . import kernels as K
 
 BF16 = torch.bfloat16
+F32 = torch.float32
 _ALIGN = 8  # elements: every segment starts 16-byte aligned
 
 
@@ -26,9 +27,20 @@ def _pad(n):
 
 
 class AdamW(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+    """torch.optim.AdamW drop-in (the reference's fused AdamW, train_gpt2.py:140-143).
+
+    master_weights=True (default): fp32 master weights and fp32 moments in arenas, the
+    model's bf16 parameters are compute copies rewritten by every step (mixed precision).
+    False: bf16 parameters and bf16 moments updated in place — the reference's own GPU
+    semantics (model.to(bfloat16) + fused AdamW), where an update below half a bf16 ulp of
+    the weight (e.g. every LayerNorm gain at lr 6e-4) rounds away.
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 master_weights: bool = True):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
+        self.master_weights = bool(master_weights)
         self._arena = None
         self._clip_coef = None
         self._step_count = 0
@@ -54,25 +66,41 @@ class AdamW(torch.optim.Optimizer):
                 total += _pad(p.numel())
             seg.append((start, total))
         total = max(total, _ALIGN)
+        sdt = F32 if self.master_weights else BF16
         parena = torch.zeros(total, dtype=BF16, device=dev)
         garena = torch.zeros(total, dtype=BF16, device=dev)
-        marena = torch.zeros(total, dtype=BF16, device=dev)
-        varena = torch.zeros(total, dtype=BF16, device=dev)
+        marena = torch.zeros(total, dtype=sdt, device=dev)
+        varena = torch.zeros(total, dtype=sdt, device=dev)
+        warena = torch.zeros(total, dtype=F32, device=dev) if self.master_weights else None
         for p, o in zip(params, offs):
             n = p.numel()
+            st = self.state[p]
             view = parena[o:o + n].view_as(p)
             view.copy_(p.data)
+            if warena is not None:
+                mview = warena[o:o + n].view_as(p)
+                # a resumed master copy (state 'master', see state_dict) beats the bf16 weight
+                mview.copy_(st["master"].to(device=dev, dtype=F32).view_as(p) if "master" in st
+                            else p.data.float())
+                st["master"] = mview
             p.data = view
             gview = garena[o:o + n].view_as(p)
             if p.grad is not None:
                 gview.copy_(p.grad)
             p.grad = gview
             p._gvl_grad_sink = True  # gvl.functional may accumulate into this grad in place
-            st = self.state[p]
-            st["step"] = torch.zeros((), dtype=torch.float32)
-            st["exp_avg"] = marena[o:o + n].view_as(p)
-            st["exp_avg_sq"] = varena[o:o + n].view_as(p)
-        self._arena = dict(p=parena, g=garena, m=marena, v=varena, offs=offs, seg=seg,
+            # state loaded before the first step (the reference resumes with
+            # configure_optimizers -> load_state_dict -> train, train_gpt2.py:320-322)
+            # moves into the arenas instead of being reset
+            for key, arena in (("exp_avg", marena), ("exp_avg_sq", varena)):
+                aview = arena[o:o + n].view_as(p)
+                if key in st:
+                    aview.copy_(st[key].to(device=dev, dtype=sdt).view_as(p))
+                st[key] = aview
+            if "step" in st:
+                self._step_count = max(self._step_count, int(float(st["step"])))
+            st["step"] = torch.tensor(float(self._step_count), dtype=torch.float32)
+        self._arena = dict(p=parena, g=garena, m=marena, v=varena, w=warena, offs=offs, seg=seg,
                            params=params)
         # per group {lr, step} on the device, read by the AdamW kernel (capturable step)
         self._hyper = torch.zeros(len(self.param_groups), 2, dtype=torch.float32, device=dev)
@@ -89,6 +117,19 @@ class AdamW(torch.optim.Optimizer):
             self._build()
         a = self._arena
         return [(p, o, p.numel()) for p, o in zip(a["params"], a["offs"])]
+
+    def master_of(self, p):
+        """fp32 master copy of parameter p (None with master_weights=False)."""
+        if self._arena is None:
+            self._build()
+        return self.state[p].get("master")
+
+    @torch.no_grad()
+    def sync_master_from_params(self):
+        """Re-seed the fp32 masters from the bf16 parameters (after the caller overwrote
+        parameters directly, e.g. model.load_state_dict after the optimizer was built)."""
+        if self._arena is not None and self._arena["w"] is not None:
+            self._arena["w"].copy_(self._arena["p"].float())
 
     def _sync_grads(self):
         """Re-point any grad that autograd replaced (e.g. after set_to_none)."""
@@ -148,9 +189,14 @@ class AdamW(torch.optim.Optimizer):
             if s1 == s0:
                 continue
             b1, b2 = g["betas"]
-            K.adamw_dev(a["p"][s0:s1], a["g"][s0:s1], a["m"][s0:s1], a["v"][s0:s1], s1 - s0,
-                        self._hyper[gi], b1, b2, g["eps"], g["weight_decay"],
-                        grad_scale=self._clip_coef)
+            if a["w"] is not None:
+                K.adamw_master_dev(a["p"][s0:s1], a["w"][s0:s1], a["g"][s0:s1], a["m"][s0:s1],
+                                   a["v"][s0:s1], s1 - s0, self._hyper[gi], b1, b2, g["eps"],
+                                   g["weight_decay"], grad_scale=self._clip_coef)
+            else:
+                K.adamw_dev(a["p"][s0:s1], a["g"][s0:s1], a["m"][s0:s1], a["v"][s0:s1], s1 - s0,
+                            self._hyper[gi], b1, b2, g["eps"], g["weight_decay"],
+                            grad_scale=self._clip_coef)
         self._clip_coef = None
         return loss
 
@@ -161,18 +207,43 @@ class AdamW(torch.optim.Optimizer):
         return super().state_dict()
 
     def load_state_dict(self, state_dict):
+        # torch casts every state tensor to its param's dtype (bf16); keep the saved fp32
+        # moments / masters at full precision instead (same param order as the groups)
+        saved_ids = [i for g in state_dict["param_groups"] for i in g["params"]]
+        mine = [p for g in self.param_groups for p in g["params"]]
+        raw = {}
+        for pid, p in zip(saved_ids, mine):
+            st = state_dict["state"].get(pid, {})
+            raw[p] = {k: v for k, v in st.items()
+                      if k in ("exp_avg", "exp_avg_sq", "master") and torch.is_tensor(v)
+                      and v.dtype == F32}
         super().load_state_dict(state_dict)
-        if self._arena is not None:
-            a = self._arena
-            for p, o in zip(a["params"], a["offs"]):
-                n = p.numel()
-                st = self.state[p]
-                for key, arena in (("exp_avg", a["m"]), ("exp_avg_sq", a["v"])):
-                    view = arena[o:o + n].view_as(p)
-                    if st[key].data_ptr() != view.data_ptr():
-                        view.copy_(st[key])
-                        st[key] = view
-                self._step_count = int(st["step"].item())
+        for p, kv in raw.items():
+            for k, v in kv.items():
+                self.state[p][k] = v.to(device=p.device)
+        if self._arena is None:
+            # moved into the arenas by _build() (first zero_grad / step)
+            steps = [int(float(st["step"])) for st in self.state.values() if "step" in st]
+            self._step_count = max(steps, default=0)
+            return
+        a = self._arena
+        steps = []
+        for p, o in zip(a["params"], a["offs"]):
+            n = p.numel()
+            st = self.state[p]
+            keys = [("exp_avg", a["m"]), ("exp_avg_sq", a["v"])]
+            if a["w"] is not None:
+                keys.append(("master", a["w"]))
+            for key, arena in keys:
+                view = arena[o:o + n].view_as(p)
+                if key in st and st[key].data_ptr() != view.data_ptr():
+                    view.copy_(st[key].to(device=view.device, dtype=view.dtype).view_as(p))
+                elif key == "master" and key not in st:
+                    view.copy_(p.data.float())
+                st[key] = view
+            if "step" in st:
+                steps.append(int(float(st["step"])))
+        self._step_count = max(steps, default=0)
 
 
 def clip_grad_norm_(optimizer_or_params, max_norm: float):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 2
+#define GVL_ABI_VERSION 3
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -152,6 +152,9 @@ int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* g, gvl_stream_
  * Logits row for target r: (r / rows_per_group) * group_stride + row_offset + r % rows_per_group
  * (lets the caption loss read logits[:, M:M+T] in place).  targets int64 with
  * ignore_index=-100; optional uint8 mask weights rows (cross-att masked mean).
+ * `vocab` need not be a multiple of 8 (GPTConfig()'s 50257): ldl / ldd are multiples of 8
+ * >= vocab rounded up to 8, and the pad columns read as -inf and get dlogits 0.  A
+ * target outside [0, vocab) (other than -100) gives row_loss NaN, never an out-of-row read.
  * Writes row_loss[r] (fp32), dlogits[r] = softmax - onehot (bf16, unscaled, 0 for
  * ignored rows, row stride ldd) and out[0]=mean loss, out[1]=1/count (count
  * clamped to >=1 when mask_mode, torch 0/0 semantics otherwise).
@@ -166,16 +169,18 @@ int gvl_cross_entropy(const void* logits, int64_t ldl, int64_t rows, int64_t voc
 /* ------------------------------------------------------------------------- */
 /* Token + position embedding gather: out[row(r)] = wte[idx[r]] + wpe[r % T],
  * row(r) = (r / T) * out_rows_per_seq + out_offset + r % T  (caption models write the
- * text embeddings after the M image tokens).
+ * text embeddings after the M image tokens).  `vocab` = rows of wte: an id outside
+ * [0, vocab) is never dereferenced (it embeds as row 0 / is dropped from the scatter);
+ * callers check ids on the host first, as nn.Embedding raises on them (ABI v3).
  * Replaces nn.Embedding x2 + add (+cat) at source/gpt2/train_gpt2.py:114-117,
  * gpt2_linear/model.py:187-200, gpt2_cross-att/model.py:155-158. */
 int gvl_embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out,
-                      int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
-                      int64_t out_offset, gvl_stream_t stream);
+                      int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
+                      int64_t out_rows_per_seq, int64_t out_offset, gvl_stream_t stream);
 /* Backward: fp32 scatter-add into dwte_acc [V][C] and dwpe_acc [T][C] (caller zeroes). */
 int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc, float* dwpe_acc,
-                      int64_t n_tokens, int64_t T, int64_t C, int64_t out_rows_per_seq,
-                      int64_t out_offset, gvl_stream_t stream);
+                      int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
+                      int64_t out_rows_per_seq, int64_t out_offset, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* CLIP token pooling: [CLS] + adaptive_avg_pool2d(side x side -> 4 x 8) + L2 normalise
@@ -204,6 +209,15 @@ int gvl_adamw(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_dec
 int gvl_adamw_dev(void* p, const void* g, void* m, void* v, int64_t n, int64_t n_decay,
                   const float* hyper, float beta1, float beta2, float eps, float weight_decay,
                   const float* grad_scale, gvl_stream_t stream);
+
+/* Mixed-precision form (gvl.optim.AdamW default): fp32 master weights p_master and fp32
+ * moments m/v are updated; the bf16 compute copy p the model reads is written from the
+ * new master (28 B/param).  Same math and device-side {lr, step} as gvl_adamw_dev.  Keeps
+ * sub-ulp updates (LayerNorm gains ~1.0: bf16 ulp 2^-7 >> lr) that a bf16-only step
+ * rounds away, so training follows the reference's fp32 path (ABI v3). */
+int gvl_adamw_master_dev(void* p, float* p_master, const void* g, float* m, float* v, int64_t n,
+                         int64_t n_decay, const float* hyper, float beta1, float beta2, float eps,
+                         float weight_decay, const float* grad_scale, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Small fused elementwise helpers on the hot path. */

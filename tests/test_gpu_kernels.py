@@ -395,7 +395,7 @@ def test_embedding_fwd_bwd(cuda):
     dout = torch.randn(B, M + T, C).to(BF)
     ate = torch.zeros(V, C, device=cuda)
     ape = torch.zeros(P, C, device=cuda)
-    K_.embedding_bwd(idx.to(cuda), dout.to(cuda), ate, ape, T, M + T, M, C)
+    K_.embedding_bwd(idx.to(cuda), dout.to(cuda), ate, ape, T, M + T, M, C, V)
     wr = wte.float().requires_grad_(True)
     pr = wpe.float().requires_grad_(True)
     ((wr[idx] + pr[:T]) * dout[:, M:].float()).sum().backward()

@@ -99,7 +99,7 @@ def inputs_lm(B, T, V, seed):
 def inputs_caption(B, L, D, T, V, seed):
     z = torch.from_numpy(W.make_normal_like(B * L * D, seed)).view(B, L, D)
     ids = torch.from_numpy(W.make_ids(B * (T + 1), V, seed + 7)).view(B, T + 1)
-    lens = torch.tensor([max(2, T - 3 * b) for b in range(B)])
+    lens = torch.tensor([max(2, T - 3 * (b % 8)) for b in range(B)])
     x, y = ids[:, :-1].clone(), ids[:, 1:].clone()
     mask = torch.arange(T).unsqueeze(0) < lens.unsqueeze(1)
     return z, x, y, mask
@@ -355,9 +355,223 @@ def fixture_full(g2, qf_mod, meta):
     np.savez(os.path.join(OUT, "full124m.npz"), **out)
 
 
+# ------------------------------------------------------------------ round-2 fixtures
+N_SAMPLE_FULL = 512
+CAP_B = 16
+
+
+def sample_tensor(key, t, out, name):
+    """Values of t at a key-determined index sample (the same sample for every quantity
+    of one parameter, so grads, params and updates line up), plus sum of squares."""
+    a = t.detach().to(torch.float64).numpy().reshape(-1)
+    out[name + "#sq"] = np.array((a * a).sum())
+    if a.size <= 4096:
+        out[name + "#full"] = a.astype(np.float32)
+    else:
+        idx = (W.make_ids(N_SAMPLE_FULL, a.size, W.key_seed(key)) % a.size).astype(np.int64)
+        out[name + "#idx"] = idx.astype(np.int32)
+        out[name + "#val"] = a[idx].astype(np.float32)
+
+
+def round_bf16_(model):
+    """Give the reference model the bf16-valued weights the GPU model holds (fp32 math):
+    'identical inputs' for the decode parity (train_gpt2.py:440-449)."""
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    return model
+
+
+def train_ref(model, micro_batches, loss_of, n_steps, lr, out, pre, names):
+    """The reference optimizer step (train_gpt2.py:457-476 / gpt2_linear/train.py:292-322):
+    zero_grad; per micro-step loss/accum + backward; clip_grad_norm_(1.0); lr; AdamW."""
+    opt = model.configure_optimizers(weight_decay=0.1, learning_rate=lr, device="cpu")
+    params = dict(model.named_parameters())
+    accum = len(micro_batches)
+    losses, norms = [], []
+    for step in range(n_steps):
+        opt.zero_grad()
+        la = 0.0
+        for mb in micro_batches:
+            loss = loss_of(model, mb) / accum
+            la += float(loss)
+            loss.backward()
+        if step == 0:
+            for n in names:
+                sample_tensor(n, params[n].grad, out, f"{pre}grad:{n}")
+        norm = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        for g in opt.param_groups:
+            g["lr"] = lr
+        opt.step()
+        losses.append(la)
+        norms.append(float(norm))
+        for n in names:
+            sample_tensor(n, params[n].data, out, f"{pre}step{step + 1}:{n}")
+    with torch.no_grad():
+        out[pre + "loss_after"] = np.array(float(loss_of(model, micro_batches[0])))
+    out[pre + "losses"] = np.array(losses)
+    out[pre + "norms"] = np.array(norms)
+
+
+def fixture_full_train(g2, lin, qf, xa, meta):
+    """Full-size (124M) training-step parity: 2 optimizer steps of the reference loop.
+    LM: 2 accumulated micro-steps of B=1x1024 each (CFG2's accumulation path at B=1);
+    linear / Q-Former / cross-att caption models at B=16 (~350 loss rows, so bf16 rounding
+    of single logits averages out as in the B=128 training batches).  lr fixed at each config's
+    max_lr (at warmup step 0 the LM update, 8.4e-7, is below bf16 resolution)."""
+    out = {}
+    cfg = g2["GPTConfig"](vocab_size=50304)
+    model = set_recipe(g2["GPT"](cfg))
+    mbs = [inputs_lm(1, 1024, 50257, s) for s in (404, 405)]
+    for i, (x, y) in enumerate(mbs):
+        out[f"lm_x{i}"], out[f"lm_y{i}"] = x.numpy(), y.numpy()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    meta["full_lm_trainable"] = names
+    train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 6e-4, out, "lm_", names)
+    print("lm", out["lm_losses"], out["lm_norms"], out["lm_loss_after"], flush=True)
+    del model
+    for kind, mod in (("linear", lin), ("qformer", qf)):
+        lm = mod.GPT_previous(mod.GPTConfig(vocab_size=50304, block_size=1024))
+        model = set_recipe(mod.GPT_Caption(enc_dim=768, lm=lm, m_vis_tokens=32))
+        model.eval()  # dropout off (SURVEY §8c); gradients still flow
+        z_raw, x, yy, mask = inputs_caption(CAP_B, 257, 768, 31, 50257, 606)
+        labels = yy.masked_fill(~mask, -100)
+        z = mod.pool_clip_197_to_33_avg_with_cls(z_raw)
+        out[f"{kind}_x"], out[f"{kind}_labels"] = x.numpy(), labels.numpy()
+        names = [n for n, p in model.named_parameters() if p.requires_grad]
+        meta[f"full_{kind}_trainable"] = names
+        train_ref(model, [(z, x, labels)], lambda m, b: m(b[0], b[1], labels=b[2])[1], 2, 1e-3,
+                  out, f"{kind}_", names)
+        print(kind, out[f"{kind}_losses"], out[f"{kind}_norms"], out[f"{kind}_loss_after"],
+              flush=True)
+        del model, lm
+    model = set_recipe(xa.GPT(xa.GPTConfig(vocab_size=50304, block_size=1024)))
+    z_raw, x, yy, mask = inputs_caption(CAP_B, 257, 768, 31, 50257, 707)
+    z = xa.pool_clip_197_to_33_avg_with_cls(z_raw)
+    out["cross_x"], out["cross_y"], out["cross_mask"] = x.numpy(), yy.numpy(), mask.numpy()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    meta["full_cross_trainable"] = names
+    train_ref(model, [(z, x, yy, mask)],
+              lambda m, b: m(b[1], z=b[0], targets=b[2], target_mask=b[3])[1], 2, 1e-3, out,
+              "cross_", names)
+    print("cross", out["cross_losses"], out["cross_norms"], out["cross_loss_after"], flush=True)
+    out["z_seeds"] = np.array([606, 707])
+    out["cap_batch"] = np.array(CAP_B)
+    np.savez_compressed(os.path.join(OUT, "full_train.npz"), **out)
+
+
+def fixture_accum(g2, qf, meta):
+    """Gradient accumulation over 4 micro-steps (the CFG2/CFG3 micro-loop, train_gpt2.py:
+    460-469) and 2 optimizer steps, tiny configs: GPT and the Q-Former caption model."""
+    out = {}
+    cfg = g2["GPTConfig"](**TINY)
+    model = set_recipe(g2["GPT"](cfg))
+    mbs = [inputs_lm(2, 48, TINY["vocab_size"], 900 + i) for i in range(4)]
+    for i, (x, y) in enumerate(mbs):
+        out[f"gpt_x{i}"], out[f"gpt_y{i}"] = x.numpy(), y.numpy()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 1e-3, out, "gpt_", names)
+    lm = qf.GPT_previous(qf.GPTConfig(**TINY))
+    model = set_recipe(qf.GPT_Caption(enc_dim=TINY["n_embd"], lm=lm, m_vis_tokens=32))
+    model.eval()
+    mbs = []
+    for i in range(4):
+        z_raw, x, yy, mask = inputs_caption(2, 257, TINY["n_embd"], 24, TINY["vocab_size"], 950 + i)
+        labels = yy.masked_fill(~mask, -100)
+        mbs.append((qf.pool_clip_197_to_33_avg_with_cls(z_raw), x, labels))
+        out[f"qformer_x{i}"], out[f"qformer_labels{i}"] = x.numpy(), labels.numpy()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    train_ref(model, mbs, lambda m, b: m(b[0], b[1], labels=b[2])[1], 2, 1e-3, out, "qformer_",
+              names)
+    out["qformer_z_seeds"] = np.array([950 + i for i in range(4)])
+    np.savez_compressed(os.path.join(OUT, "accum_tiny.npz"), **out)
+
+
+def fixture_edge(lin, qf, xa, meta):
+    """Reference edge cases: use_cls_only (M=1; Q-Former cross-attention over Tk=1),
+    2-D patch_tokens, M+T > block_size truncation (gpt2_linear/model.py:181-196), and the
+    cross-att GPT with z=None (gpt2_cross-att/model.py:159-165)."""
+    out = {}
+    z_raw, x, yy, mask = inputs_caption(2, 257, TINY["n_embd"], 24, TINY["vocab_size"], 202)
+    labels = yy.masked_fill(~mask, -100)
+    ids_long = torch.from_numpy(W.make_ids(2 * 41, TINY["vocab_size"], 808)).view(2, 41)
+    x_long, y_long = ids_long[:, :-1].clone(), ids_long[:, 1:].clone()
+    out["x_long"], out["y_long"] = x_long.numpy(), y_long.numpy()
+    for kind, mod in (("linear", lin), ("qformer", qf)):
+        z = mod.pool_clip_197_to_33_avg_with_cls(z_raw)
+        cases = {
+            "cls": (dict(use_cls_only=True), lambda m: m(z, x, labels=labels)),
+            "patch2d": (dict(), lambda m: m(z[:, 0], x, labels=labels)),
+            "trunc": (dict(), lambda m: m(z, x_long, labels=y_long)),
+        }
+        for case, (kw, fn) in cases.items():
+            lm = mod.GPT_previous(mod.GPTConfig(**TINY))
+            model = set_recipe(mod.GPT_Caption(enc_dim=TINY["n_embd"], lm=lm, m_vis_tokens=32, **kw))
+            model.eval()
+            logits, loss = fn(model)
+            loss.backward()
+            pre = f"{kind}_{case}_"
+            out[pre + "loss"] = np.array(float(loss))
+            out[pre + "logits_shape"] = np.array(logits.shape)
+            out[pre + "logits_sq"] = np.array(float((logits.double() ** 2).sum()))
+            for n, p in model.named_parameters():
+                if p.requires_grad:
+                    sample_tensor(n, p.grad, out, pre + "grad:" + n)
+            print(pre, float(loss), tuple(logits.shape), flush=True)
+    model = set_recipe(xa.GPT(xa.GPTConfig(**TINY, img_embd=TINY["n_embd"])))
+    logits, loss = model(x, z=None, targets=yy)
+    out["cross_noz_loss"] = np.array(float(loss))
+    out["cross_noz_logits_sq"] = np.array(float((logits.double() ** 2).sum()))
+    out["x"], out["y"], out["labels"] = x.numpy(), yy.numpy(), labels.numpy()
+    out["z_seed"] = np.array(202)
+    np.savez_compressed(os.path.join(OUT, "edge_tiny.npz"), **out)
+
+
+def fixture_greedy(g2, lin, qf, xa, meta):
+    """Greedy decode of the reference models on the bf16-valued weights the GPU model
+    holds (fp32 math): tiny configs of all four models and the full-size 124M LM, linear,
+    Q-Former and cross-att models.  16 new tokens each, with top-1/top-2 margins."""
+    out = {}
+
+    def run(pre, fn, prompt):
+        toks, margins = greedy(fn, prompt, 16)
+        out[pre + "prompt"] = prompt.numpy()
+        out[pre + "tokens"] = toks.numpy()
+        out[pre + "margins"] = margins.numpy()
+        print(pre, toks.tolist(), np.round(margins.numpy(), 3).tolist(), flush=True)
+
+    for size, cfg_kw, B_lm in (("tiny", TINY, None), ("full", dict(vocab_size=50304), None)):
+        V = cfg_kw.get("vocab_size")
+        D = cfg_kw.get("n_embd", 768)
+        model = round_bf16_(set_recipe(g2["GPT"](g2["GPTConfig"](**cfg_kw))))
+        x, _ = inputs_lm(1, 24, min(V, 50257), 1111)
+        run(f"{size}_gpt_", lambda s: model(s)[0], x[:, :8])
+        z_raw, xc, _, _ = inputs_caption(1, 257, D, 8, min(V, 50257), 1212)
+        for kind, mod in (("linear", lin), ("qformer", qf)):
+            c = dict(cfg_kw)
+            c.setdefault("block_size", 1024)
+            lm = mod.GPT_previous(mod.GPTConfig(**c))
+            m = round_bf16_(set_recipe(mod.GPT_Caption(enc_dim=D, lm=lm, m_vis_tokens=32)))
+            m.eval()
+            z = mod.pool_clip_197_to_33_avg_with_cls(z_raw)
+            run(f"{size}_{kind}_", lambda s: m(z, s)[0], xc[:, :3])
+        c = dict(cfg_kw)
+        if size == "tiny":
+            c["img_embd"] = D
+        m = round_bf16_(set_recipe(xa.GPT(xa.GPTConfig(**c))))
+        z = xa.pool_clip_197_to_33_avg_with_cls(z_raw)
+        run(f"{size}_cross_", lambda s: m(s, z=z)[0], xc[:, :3])
+        del model, m
+    out["z_seed"] = np.array(1212)
+    np.savez_compressed(os.path.join(OUT, "greedy.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also the 124M scalar fixtures")
+    ap.add_argument("--only", default="",
+                    help="comma list of round-2 sets to (re)generate alone: "
+                         "full_train,accum,edge,greedy")
     args = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(os.cpu_count() or 8)
@@ -367,6 +581,19 @@ def main():
     lin = load_module("gpt2_linear", "ref_gpt2_linear_model")
     qf = load_module("gpt2_q_former", "ref_gpt2_q_former_model")
     xa = load_module("gpt2_cross-att", "ref_gpt2_cross_att_model")
+    if args.only:
+        mpath = os.path.join(OUT, "meta.json")
+        with open(mpath) as f:
+            meta = json.load(f)
+        sets = {"full_train": lambda: fixture_full_train(g2, lin, qf, xa, meta),
+                "accum": lambda: fixture_accum(g2, qf, meta),
+                "edge": lambda: fixture_edge(lin, qf, xa, meta),
+                "greedy": lambda: fixture_greedy(g2, lin, qf, xa, meta)}
+        for name in args.only.split(","):
+            sets[name]()
+        with open(mpath, "w") as f:
+            json.dump(meta, f, indent=1)
+        return
     fixture_ops(lin)
     fixture_gpt(g2, meta)
     fixture_caption(lin, "linear", meta, m_vis=32)
