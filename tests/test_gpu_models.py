@@ -8,8 +8,8 @@ Tolerances (documented in DESIGN.md §5):
   * gradients: 1.2e-1 of the tensor's max magnitude against the fp32-weight reference
     (bf16 weight rounding + bf16 dS in attention backward dominate; the deepest chain, the
     cross-attention q_proj gradient, shows ~9e-2); parameters after 3 AdamW steps: 8e-2;
-  * greedy decode: identical tokens for every step whose fp32 top-1/top-2 margin exceeds
-    the bf16 bound (0.05 logits here); the comparison stops at the first near-tie.
+  * greedy decode: tests/test_gpu_parity_full.py (every token vs the reference's own
+    tokens on the same bf16-valued weights, tiny and full size).
 """
 import numpy as np
 import pytest
@@ -113,54 +113,6 @@ def test_three_adamw_steps(cuda, golden, meta, kind):
     params = dict(m.named_parameters())
     for n in named_trainable(kind, meta):
         check_summary(fx, "step3:" + n, params[n].float(), 8e-2)
-
-
-@pytest.mark.parametrize("kind", ["gpt", "linear", "qformer", "cross"])
-def test_greedy_decode(cuda, golden, meta, kind):
-    from gvl.generate import greedy_caption, greedy_lm
-    fx = golden(f"{kind}_tiny")
-    m = _model(kind, meta, cuda)
-    prompt = torch.from_numpy(fx["greedy_prompt"]).to(cuda)
-    if kind == "gpt":
-        toks, _ = greedy_lm(m, prompt, 16)
-    else:
-        from gvl.caption import pool_clip_197_to_33_avg_with_cls as pool
-        z = pool(torch.from_numpy(fx["z_raw"]).to(cuda))[:1]
-        if kind == "cross":
-            toks, _ = greedy_lm(m, prompt, 16, z=z)
-        else:
-            toks, _ = greedy_caption(m, z, prompt, 16)
-    # the reference CPU path on identical inputs: oracle (fp32 math) on the same
-    # bf16-valued weights the GPU model holds
-    from oracle import models as OM
-    from oracle import ops as O
-    P = {k: v.to(BF).float() for k, v in recipe_params(meta[f"{kind}_keys"]).items()}
-    pc = prompt.cpu()
-    if kind == "gpt":
-        fn = lambda s: OM.gpt_forward(P, s, 2, 2)[0]
-    elif kind == "cross":
-        zc = O.pool_clip(torch.from_numpy(fx["z_raw"]))[:1]
-        fn = lambda s: OM.cross_att_forward(P, s, zc, 2, 2)[0]
-    else:
-        zc = O.pool_clip(torch.from_numpy(fx["z_raw"]))[:1]
-        fn = lambda s: OM.caption_forward(P, kind, zc, s, 2, 2, 64)[0]
-    want, marg = OM.greedy(fn, pc, 16)
-    want, marg = want[0].numpy(), marg[0].numpy()
-    got = toks[0].cpu().numpy()
-    bound = 0.02
-    n_ok = 0
-    for i in range(len(want)):
-        if marg[i] < bound:  # near-tie: a flip is legitimate; sequences then diverge
-            if got[i] != want[i]:
-                break
-            continue
-        assert got[i] == want[i], (f"{kind}: token {i} differs ({got[i]} vs {want[i]}), "
-                                   f"margin {marg[i]:.4f}; margins {np.round(marg, 4)}")
-        n_ok += 1
-    ref_fx = fx["greedy_tokens"][0]
-    print(f"{kind}: {n_ok} greedy tokens bit-exact vs oracle(bf16 weights); margins "
-          f"{np.round(marg, 4)}; fp32-weight reference tokens {ref_fx.tolist()} got {got.tolist()}")
-    assert n_ok >= 4
 
 
 def test_grad_accumulation_equivalence(cuda, meta, golden):

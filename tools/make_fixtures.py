@@ -382,9 +382,37 @@ def round_bf16_(model):
     return model
 
 
-def train_ref(model, micro_batches, loss_of, n_steps, lr, out, pre, names):
+class _Bf16Weights:
+    """Run the enclosed forward/backward on bf16-rounded copies of the (fp32 master)
+    weights, restoring the masters afterwards: the mixed-precision loop gvl trains with
+    (bf16 compute weights, fp32 master weights + moments), with the reference's own model
+    code and autograd computing every loss and gradient."""
+
+    def __init__(self, model, on):
+        self.model, self.on = model, on
+
+    def __enter__(self):
+        if self.on:
+            self.saved = [p.detach().clone() for p in self.model.parameters()]
+            with torch.no_grad():
+                for p in self.model.parameters():
+                    p.copy_(p.to(torch.bfloat16).float())
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            with torch.no_grad():
+                for p, s in zip(self.model.parameters(), self.saved):
+                    p.copy_(s)
+
+
+def train_ref(model, micro_batches, loss_of, n_steps, lr, out, pre, names, mp=False):
     """The reference optimizer step (train_gpt2.py:457-476 / gpt2_linear/train.py:292-322):
-    zero_grad; per micro-step loss/accum + backward; clip_grad_norm_(1.0); lr; AdamW."""
+    zero_grad; per micro-step loss/accum + backward; clip_grad_norm_(1.0); lr; AdamW.
+    mp=True: the same loop in mixed precision (_Bf16Weights), masters starting at the
+    bf16-rounded initial weights — identical inputs to the GPU model at every step."""
+    if mp:
+        round_bf16_(model)
     opt = model.configure_optimizers(weight_decay=0.1, learning_rate=lr, device="cpu")
     params = dict(model.named_parameters())
     accum = len(micro_batches)
@@ -392,10 +420,11 @@ def train_ref(model, micro_batches, loss_of, n_steps, lr, out, pre, names):
     for step in range(n_steps):
         opt.zero_grad()
         la = 0.0
-        for mb in micro_batches:
-            loss = loss_of(model, mb) / accum
-            la += float(loss)
-            loss.backward()
+        with _Bf16Weights(model, mp):
+            for mb in micro_batches:
+                loss = loss_of(model, mb) / accum
+                la += float(loss.detach())
+                loss.backward()
         if step == 0:
             for n in names:
                 sample_tensor(n, params[n].grad, out, f"{pre}grad:{n}")
@@ -407,7 +436,7 @@ def train_ref(model, micro_batches, loss_of, n_steps, lr, out, pre, names):
         norms.append(float(norm))
         for n in names:
             sample_tensor(n, params[n].data, out, f"{pre}step{step + 1}:{n}")
-    with torch.no_grad():
+    with torch.no_grad(), _Bf16Weights(model, mp):
         out[pre + "loss_after"] = np.array(float(loss_of(model, micro_batches[0])))
     out[pre + "losses"] = np.array(losses)
     out[pre + "norms"] = np.array(norms)
@@ -429,6 +458,9 @@ def fixture_full_train(g2, lin, qf, xa, meta):
     meta["full_lm_trainable"] = names
     train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 6e-4, out, "lm_", names)
     print("lm", out["lm_losses"], out["lm_norms"], out["lm_loss_after"], flush=True)
+    model = set_recipe(g2["GPT"](cfg))
+    train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 6e-4, out, "mp_lm_", names, mp=True)
+    print("mp lm", out["mp_lm_losses"], out["mp_lm_norms"], out["mp_lm_loss_after"], flush=True)
     del model
     for kind, mod in (("linear", lin), ("qformer", qf)):
         lm = mod.GPT_previous(mod.GPTConfig(vocab_size=50304, block_size=1024))
@@ -440,10 +472,14 @@ def fixture_full_train(g2, lin, qf, xa, meta):
         out[f"{kind}_x"], out[f"{kind}_labels"] = x.numpy(), labels.numpy()
         names = [n for n, p in model.named_parameters() if p.requires_grad]
         meta[f"full_{kind}_trainable"] = names
-        train_ref(model, [(z, x, labels)], lambda m, b: m(b[0], b[1], labels=b[2])[1], 2, 1e-3,
-                  out, f"{kind}_", names)
-        print(kind, out[f"{kind}_losses"], out[f"{kind}_norms"], out[f"{kind}_loss_after"],
-              flush=True)
+        for pre, mp in ((f"{kind}_", False), (f"mp_{kind}_", True)):
+            lm = mod.GPT_previous(mod.GPTConfig(vocab_size=50304, block_size=1024))
+            model = set_recipe(mod.GPT_Caption(enc_dim=768, lm=lm, m_vis_tokens=32))
+            model.eval()
+            train_ref(model, [(z, x, labels)], lambda m, b: m(b[0], b[1], labels=b[2])[1], 2,
+                      1e-3, out, pre, names, mp=mp)
+            print(pre, out[pre + "losses"], out[pre + "norms"], out[pre + "loss_after"],
+                  flush=True)
         del model, lm
     model = set_recipe(xa.GPT(xa.GPTConfig(vocab_size=50304, block_size=1024)))
     z_raw, x, yy, mask = inputs_caption(CAP_B, 257, 768, 31, 50257, 707)
@@ -451,10 +487,12 @@ def fixture_full_train(g2, lin, qf, xa, meta):
     out["cross_x"], out["cross_y"], out["cross_mask"] = x.numpy(), yy.numpy(), mask.numpy()
     names = [n for n, p in model.named_parameters() if p.requires_grad]
     meta["full_cross_trainable"] = names
-    train_ref(model, [(z, x, yy, mask)],
-              lambda m, b: m(b[1], z=b[0], targets=b[2], target_mask=b[3])[1], 2, 1e-3, out,
-              "cross_", names)
-    print("cross", out["cross_losses"], out["cross_norms"], out["cross_loss_after"], flush=True)
+    for pre, mp in (("cross_", False), ("mp_cross_", True)):
+        model = set_recipe(xa.GPT(xa.GPTConfig(vocab_size=50304, block_size=1024)))
+        train_ref(model, [(z, x, yy, mask)],
+                  lambda m, b: m(b[1], z=b[0], targets=b[2], target_mask=b[3])[1], 2, 1e-3, out,
+                  pre, names, mp=mp)
+        print(pre, out[pre + "losses"], out[pre + "norms"], out[pre + "loss_after"], flush=True)
     out["z_seeds"] = np.array([606, 707])
     out["cap_batch"] = np.array(CAP_B)
     np.savez_compressed(os.path.join(OUT, "full_train.npz"), **out)
@@ -462,7 +500,8 @@ def fixture_full_train(g2, lin, qf, xa, meta):
 
 def fixture_accum(g2, qf, meta):
     """Gradient accumulation over 4 micro-steps (the CFG2/CFG3 micro-loop, train_gpt2.py:
-    460-469) and 2 optimizer steps, tiny configs: GPT and the Q-Former caption model."""
+    460-469) and 2 optimizer steps, tiny configs: GPT and the Q-Former caption model
+    (mixed-precision loop: bf16 compute weights, fp32 masters — train_ref(mp=True))."""
     out = {}
     cfg = g2["GPTConfig"](**TINY)
     model = set_recipe(g2["GPT"](cfg))
@@ -470,7 +509,7 @@ def fixture_accum(g2, qf, meta):
     for i, (x, y) in enumerate(mbs):
         out[f"gpt_x{i}"], out[f"gpt_y{i}"] = x.numpy(), y.numpy()
     names = [n for n, p in model.named_parameters() if p.requires_grad]
-    train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 1e-3, out, "gpt_", names)
+    train_ref(model, mbs, lambda m, b: m(b[0], b[1])[1], 2, 1e-3, out, "gpt_", names, mp=True)
     lm = qf.GPT_previous(qf.GPTConfig(**TINY))
     model = set_recipe(qf.GPT_Caption(enc_dim=TINY["n_embd"], lm=lm, m_vis_tokens=32))
     model.eval()
@@ -482,7 +521,7 @@ def fixture_accum(g2, qf, meta):
         out[f"qformer_x{i}"], out[f"qformer_labels{i}"] = x.numpy(), labels.numpy()
     names = [n for n, p in model.named_parameters() if p.requires_grad]
     train_ref(model, mbs, lambda m, b: m(b[0], b[1], labels=b[2])[1], 2, 1e-3, out, "qformer_",
-              names)
+              names, mp=True)
     out["qformer_z_seeds"] = np.array([950 + i for i in range(4)])
     np.savez_compressed(os.path.join(OUT, "accum_tiny.npz"), **out)
 
