@@ -161,7 +161,9 @@ def kernel_pass(step, first_it, steps, timer):
 
 
 def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
-    from gvl import kernels as K
+    """Time exactly `steps` steps (barrier + synchronize on both sides, max over ranks);
+    then, outside the timed region, one eager kernel pass of `kernel_steps` steps with the
+    per-GEMM dispatch timer (the roofline line)."""
     eager = step
     if graph:
         step = graphed(step, warmup)
@@ -172,8 +174,6 @@ def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if timer is not None and not graph:
-        K.set_kernel_timer(timer)
     t0 = time.perf_counter()
     r = None
     for i in range(steps):
@@ -183,14 +183,14 @@ def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    K.set_kernel_timer(None)
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    if graph and timer is not None:
+    loss, norm = float(r.loss), float(r.norm)  # read before the kernel pass moves the model
+    if timer is not None:
         kernel_pass(eager, warmup + steps, kernel_steps, timer)
-    return dt, r
+    return dt, (loss, norm)
 
 
 TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
@@ -208,27 +208,69 @@ def pmc_traffic(workload, kernel):
         return None
 
 
-def dominant_kernel(summary, workload="lm"):
+def dominant_kernel(summary, workload="lm", steps=1):
+    """Roofline of the GEMM instance with the largest total time.  Durations come from HIP
+    events bound to each kernel's own dispatch (gvl.kernels.KernelTimer, dispatch=True):
+    the interval rocprofv3's kernel trace reports for the same kernel name.  Also lists the
+    top GEMM instances (per-step launches, average duration, fraction of peak)."""
     name, s = max(summary.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = s["ms"] / s["launches"]
     achieved = s["flops"] / (s["ms"] * 1e-3) / 1e12
+    top = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:6]
+    table = [dict(kernel=k, launches_per_step=round(v["launches"] / steps, 2),
+                  ms_per_step=round(v["ms"] / steps, 3),
+                  avg_us=round(v["ms"] / v["launches"] * 1e3, 2),
+                  frac=round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4))
+             for k, v in top]
     return dict(kernel=name, bound="mfma", achieved=round(achieved, 1), peak=PEAK_BF16_TFLOPS,
                 unit="TFLOP/s", frac=round(achieved / PEAK_BF16_TFLOPS, 4),
                 traffic=pmc_traffic(workload, name), traffic_unit="bytes/launch",
                 launches=s["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 avg_flop_per_launch=s["flops"] / s["launches"],
+                timing="hip events bound to the kernel dispatch (hipExtLaunchKernelGGL), "
+                       "eager pass of the same step",
                 all_gemm_frac=round(sum(v["flops"] for v in summary.values())
                                     / (sum(v["ms"] for v in summary.values()) * 1e-3) / 1e12
-                                    / PEAK_BF16_TFLOPS, 4))
+                                    / PEAK_BF16_TFLOPS, 4),
+                gemm_ms_per_step=round(sum(v["ms"] for v in summary.values()) / steps, 3),
+                top_gemms=table)
 
 
 # ---------------------------------------------------------------------- CPU baseline
-def cpu_baseline(workload, seconds=15.0):
-    """The oracle (fp32 CPU restatement of the reference step) on this host's cores:
-    zero_grad -> fwd -> bwd -> clip -> AdamW on a bounded sample (LM: B=1 x 1024 tokens;
-    caption: B=8 images), repeated until ~`seconds` of CPU work."""
+def host_threads():
+    """Threads this process may use: the affinity mask (the GPU box's share; os.cpu_count()
+    there reports the whole machine), capped by OMP_NUM_THREADS when set."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(workload, seconds=15.0, max_steps=6):
+    """The oracle (fp32 CPU restatement of the reference step, pinned to the reference's
+    fixtures) on this host's cores: zero_grad -> fwd -> bwd -> clip -> AdamW, repeated for
+    ~`seconds` of CPU work.  Sample: LM = BASELINE configs[0] itself (B=4 x T=1024);
+    captions = B=32 images of the B=128 step (z (32,257,768) pooled, 31 text tokens)."""
     from oracle import models as OM
-    threads = min(16, os.cpu_count() or 1)
+    from oracle import ops as O
+    O.FAST_PATHS = True  # the torch ops the reference itself calls (oracle/ops.py)
+    threads = host_threads()
     torch.set_num_threads(threads)
     import gvl.gpt2 as g2
     with torch.device("meta"):
@@ -240,38 +282,41 @@ def cpu_baseline(workload, seconds=15.0):
     g = torch.Generator().manual_seed(0)
     P = {k: torch.randn(s, generator=g) * 0.02 for k, s in keys}
     if workload == "lm":
+        B = 4
         P["transformer.wte.weight"] = P["lm_head.weight"]
-        ids = torch.randint(0, 50257, (1, 1025), generator=g)
-        x, y = ids[:, :-1], ids[:, 1:]
-        kind, units_per_step, unit = "gpt", 1024, "tokens/s"
+        ids = torch.randint(0, 50257, (B * 1024 + 1,), generator=g)
+        x, y = ids[:-1].view(B, 1024), ids[1:].view(B, 1024)
+        kind, units_per_step, unit = "gpt", B * 1024, "tokens/s"
         train = OM.trainable_keys("gpt", list(P))
         loss_of = lambda P_, it: OM.gpt_forward(P_, x, 12, 12, y)[1]
-        sample = "GPT-2 124M LM step, B=1 x T=1024 (fp32, oracle restatement)"
+        sample = f"GPT-2 124M LM step, B={B} x T=1024 (configs[0]; fp32 oracle restatement)"
     else:
         from gvl.train import caption_batch, caption_labels
         from oracle import ops as O
-        z, xx, yy, mm = caption_batch(8, device="cpu")
+        B = 32
+        z, xx, yy, mm = caption_batch(B, device="cpu")
         zp = O.pool_clip(z)
         lab = caption_labels(yy, mm)
-        P["gpt.transformer.wte.weight"] = P["gpt.lm_head.weight"]
         kind = {"qformer": "qformer", "linear": "linear"}.get(workload, "cross")
-        units_per_step, unit = 8, "images/s"
+        units_per_step, unit = B, "images/s"
         train = OM.trainable_keys(kind, list(P))
         if kind == "cross":
+            P["transformer.wte.weight"] = P["lm_head.weight"]
             loss_of = lambda P_, it: OM.cross_att_forward(P_, xx, zp, 12, 12, yy, mm)[1]
         else:
+            P["gpt.transformer.wte.weight"] = P["gpt.lm_head.weight"]
             loss_of = lambda P_, it: OM.caption_forward(P_, kind, zp, xx, 12, 12, 1024, lab)[1]
-        sample = f"{workload} caption step, B=8 images (fp32, oracle restatement)"
+        sample = f"{workload} caption step, B={B} images (fp32 oracle restatement)"
     OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
         OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)
         n += 1
-        if time.perf_counter() - t0 > seconds or n >= 20:
+        if time.perf_counter() - t0 > seconds or n >= max_steps:
             break
     dt = time.perf_counter() - t0
     return dict(value=round(units_per_step * n / dt, 2), unit=unit, cores=threads, kind="port",
-                sample=f"{sample}; {n} steps in {dt:.1f}s")
+                cpu=cpu_model(), sample=f"{sample}; {n} steps in {dt:.1f}s")
 
 
 def build_caption_meta(kind):
@@ -298,6 +343,12 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--caption-steps", type=int, default=10)
+    ap.add_argument("--captions", default="qformer,linear,cross",
+                    help="secondary caption-step lines of the default (lm) run")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU work per cpu_baseline sample (LM; captions get half)")
+    ap.add_argument("--no-kernel-pass", action="store_true",
+                    help="skip the eager per-GEMM timing pass (profiling runs)")
     ap.add_argument("--no-graph", action="store_true",
                     help="eager steps (default at N=1: the step is captured into one hipGraph)")
     args = ap.parse_args()
@@ -314,10 +365,10 @@ def main():
         step, units, cfg = run_caption(args.workload, args, world, rank, dev)
         unit, flop_per_unit = "images/s", CAP_FLOP_PER_IMAGE[args.workload]
     use_graph = world == 1 and not args.no_graph
-    timer = K.KernelTimer()
+    timer = None if args.no_kernel_pass else K.KernelTimer()
     dt, res = timed(step, args.steps, args.warmup, world, timer, graph=use_graph)
     value = units * args.steps / dt
-    roof = dominant_kernel(timer.summary(), args.workload)
+    roof = dominant_kernel(timer.summary(), args.workload, steps=1) if timer else None
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -326,24 +377,35 @@ def main():
         "dtype": "bf16", "data": "synthetic (random tokens / N(0,1) CLIP tokens), random-init weights",
         "config": dict(cfg, model="gpt2-124m", parallelism=f"dp{world}"),
         "step_mfma_frac": round(value * flop_per_unit / 1e12 / PEAK_BF16_TFLOPS / world, 4),
-        "loss": round(float(res.loss), 5), "grad_norm": round(float(res.norm), 5),
+        "loss": round(res[0], 5), "grad_norm": round(res[1], 5),
         "hip_graph": use_graph,
         "roofline": roof,
     }
     if args.workload == "lm" and not args.no_secondary:
         del step
         torch.cuda.empty_cache()
-        cstep, cunits, ccfg = run_caption("qformer", args, world, rank, dev)
-        ctimer = K.KernelTimer()
-        cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer, graph=use_graph,
-                          kernel_steps=3)
-        cval = cunits * args.caption_steps / cdt
-        out["caption_qformer"] = dict(
-            value=round(cval, 1), unit="images/s", ms_per_step=round(cdt / args.caption_steps * 1e3, 3),
-            step_mfma_frac=round(cval * CAP_FLOP_PER_IMAGE["qformer"] / 1e12 / PEAK_BF16_TFLOPS / world, 4),
-            loss=round(float(cres.loss), 5), config=ccfg, roofline=dominant_kernel(ctimer.summary(), "qformer"))
+        for kind in args.captions.split(","):
+            if not kind:
+                continue
+            cstep, cunits, ccfg = run_caption(kind, args, world, rank, dev)
+            ctimer = None if args.no_kernel_pass else K.KernelTimer()
+            cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer, graph=use_graph,
+                              kernel_steps=3)
+            cval = cunits * args.caption_steps / cdt
+            line = dict(
+                value=round(cval, 1), unit="images/s",
+                ms_per_step=round(cdt / args.caption_steps * 1e3, 3),
+                step_mfma_frac=round(cval * CAP_FLOP_PER_IMAGE[kind] / 1e12 / PEAK_BF16_TFLOPS
+                                     / world, 4),
+                loss=round(cres[0], 5), config=ccfg,
+                roofline=dominant_kernel(ctimer.summary(), kind, steps=3) if ctimer else None)
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                line["cpu_baseline"] = cpu_baseline(kind, seconds=args.cpu_seconds / 2)
+            out[f"caption_{kind}"] = line
+            del cstep
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.workload)
+        out["cpu_baseline"] = cpu_baseline(args.workload, seconds=args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -638,11 +638,11 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   dim3 grid(grid_1d(d, (d->Tq + 64 * G - 1) / (64 * G)));
   hipStream_t s = gvl::as_stream(stream);
   if (G == 2) {
-    if (p.has_drop) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(NT), 0, s, p);
-    else hipLaunchKernelGGL((attn_fwd_kernel<2, false>), grid, dim3(NT), 0, s, p);
+    if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
+    else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
   } else {
-    if (p.has_drop) hipLaunchKernelGGL((attn_fwd_kernel<1, true>), grid, dim3(NT), 0, s, p);
-    else hipLaunchKernelGGL((attn_fwd_kernel<1, false>), grid, dim3(NT), 0, s, p);
+    if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true>, grid, dim3(NT), 0, s, p);
+    else gvl::launch_timed(attn_fwd_kernel<1, false>, grid, dim3(NT), 0, s, p);
   }
   GVL_LAUNCH_CHECK("gvl_attn_fwd");
   return 0;

@@ -6,6 +6,7 @@
 
 namespace {
 thread_local std::string g_last_error;
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
 }
 
 namespace gvl {
@@ -31,6 +32,14 @@ int num_cus() {
   return cached[dev];
 }
 
+bool take_launch_events(hipEvent_t* start, hipEvent_t* stop) {
+  if (!g_ev_start || !g_ev_stop) return false;
+  *start = g_ev_start;
+  *stop = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+  return true;
+}
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -44,4 +53,9 @@ int check_launch(const char* what) {
 extern "C" {
 const char* gvl_last_error(void) { return g_last_error.c_str(); }
 int gvl_abi_version(void) { return GVL_ABI_VERSION; }
+int gvl_set_launch_events(void* start, void* stop) {
+  g_ev_start = reinterpret_cast<hipEvent_t>(start);
+  g_ev_stop = reinterpret_cast<hipEvent_t>(stop);
+  return 0;
+}
 }

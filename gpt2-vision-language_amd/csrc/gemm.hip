@@ -285,10 +285,10 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   p.tiles_m = (int)((d->m + BM - 1) / BM);
   p.tiles_n = (int)((d->n + BN - 1) / BN);
   const int grid = p.tiles_m * p.tiles_n;
-  if (!d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, false>), dim3(grid), dim3(NT), 0, s, p);
-  else if (!d->a_mn && d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<false, true>), dim3(grid), dim3(NT), 0, s, p);
-  else if (d->a_mn && !d->b_mn) hipLaunchKernelGGL((gemm_bf16_kernel<true, false>), dim3(grid), dim3(NT), 0, s, p);
-  else hipLaunchKernelGGL((gemm_bf16_kernel<true, true>), dim3(grid), dim3(NT), 0, s, p);
+  if (!d->a_mn && !d->b_mn) gvl::launch_timed(gemm_bf16_kernel<false, false>, dim3(grid), dim3(NT), 0, s, p);
+  else if (!d->a_mn && d->b_mn) gvl::launch_timed(gemm_bf16_kernel<false, true>, dim3(grid), dim3(NT), 0, s, p);
+  else if (d->a_mn && !d->b_mn) gvl::launch_timed(gemm_bf16_kernel<true, false>, dim3(grid), dim3(NT), 0, s, p);
+  else gvl::launch_timed(gemm_bf16_kernel<true, true>, dim3(grid), dim3(NT), 0, s, p);
   GVL_LAUNCH_CHECK("gvl_gemm");
   return 0;
 }

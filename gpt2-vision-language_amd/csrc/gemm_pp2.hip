@@ -143,7 +143,7 @@ int launch_pp2(const GemmP& p0, hipStream_t s) {
   }
   p.kper = p.splits > 1 ? ((p.K / p.splits + KS - 1) / KS) * KS : p.K;
   if (p.splits > 1) p.splits = (int)((p.K + p.kper - 1) / p.kper);
-  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(512), lds, s, p);
+  gvl::launch_timed(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(512), lds, s, p);
   if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }
@@ -315,7 +315,7 @@ int launch_pp3(const GemmP& p0, hipStream_t s) {
   }
   const int total = p.tiles_m * p.tiles_n * p.splits;
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, p);
+  gvl::launch_timed(kern, dim3(grid), dim3(512), lds, s, p);
   if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }

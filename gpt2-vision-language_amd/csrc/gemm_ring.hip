@@ -278,7 +278,7 @@ int launch_pp(const GemmP& p0, hipStream_t s) {
   }
   p.kper = p.splits > 1 ? ((p.K / p.splits + KS - 1) / KS) * KS : p.K;
   if (p.splits > 1) p.splits = (int)((p.K + p.kper - 1) / p.kper);
-  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(512), lds, s, p);
+  gvl::launch_timed(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(512), lds, s, p);
   if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }
@@ -302,7 +302,7 @@ int launch_cfg(const GemmP& p0, hipStream_t s) {
   }
   p.kper = p.splits > 1 ? ((p.K / p.splits + KS - 1) / KS) * KS : p.K;
   if (p.splits > 1) p.splits = (int)((p.K + p.kper - 1) / p.kper);
-  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(64 * WMW * WNW), lds, s, p);
+  gvl::launch_timed(kern, dim3(p.tiles_m * p.tiles_n * p.splits), dim3(64 * WMW * WNW), lds, s, p);
   if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }

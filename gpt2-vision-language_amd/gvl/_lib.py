@@ -67,6 +67,7 @@ class AttnBwdDesc(C.Structure):
 SIGNATURES = {
     "gvl_last_error": (C.c_char_p, []),
     "gvl_abi_version": (C.c_int, []),
+    "gvl_set_launch_events": (C.c_int, [c_vp, c_vp]),
     "gvl_gemm": (C.c_int, [C.POINTER(GemmDesc), c_vp]),
     "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
     "gvl_gemm_kernel_name": (C.c_int, [C.POINTER(GemmDesc), C.c_char_p, c_i32]),

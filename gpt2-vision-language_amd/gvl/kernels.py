@@ -46,11 +46,16 @@ def _rowmajor(t, name):
 
 # ------------------------------------------------------------------ live kernel timing
 class KernelTimer:
-    """Brackets every GEMM launch with HIP events on the launch stream (bench.py uses it
-    over its timed region to report the dominant kernel's achieved TFLOP/s)."""
+    """Times every GEMM launch with a pair of HIP events (bench.py's roofline line).
 
-    def __init__(self):
+    dispatch=True (default): the events are bound to the GEMM kernel's own dispatch
+    (gvl_set_launch_events -> hipExtLaunchKernelGGL), so each interval is the kernel's
+    execution as its dispatch records it — the quantity rocprofv3's kernel trace reports.
+    dispatch=False: two stream markers around the launch (includes dispatch latency)."""
+
+    def __init__(self, dispatch: bool = True):
         self.records = []
+        self.dispatch = dispatch
 
     def summary(self):
         torch.cuda.synchronize()
@@ -149,9 +154,18 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     if _timer is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
-        e1.record()
+        if _timer.dispatch:
+            e0.record()  # materialise both hipEvents; the launch re-records them
+            e1.record()
+            _L().gvl_set_launch_events(C.c_void_p(e0.cuda_event), C.c_void_p(e1.cuda_event))
+            try:
+                _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
+            finally:
+                _L().gvl_set_launch_events(None, None)
+        else:
+            e0.record()
+            _lib.check(_L().gvl_gemm(C.byref(d), _stream()), "gvl_gemm")
+            e1.record()
         buf = C.create_string_buffer(128)
         _L().gvl_gemm_kernel_name(C.byref(d), buf, 128)
         _timer.records.append((buf.value.decode(), e0, e1, 2.0 * M * N * K))

@@ -38,6 +38,12 @@ typedef void* gvl_stream_t;
 
 const char* gvl_last_error(void);
 int gvl_abi_version(void);
+/* Measurement hook (bench.py roofline): arm a (start, stop) pair of timing-enabled
+ * hipEvent_t for the calling thread; the main kernel of the next gvl_gemm / gvl_attn_fwd /
+ * gvl_attn_bwd call on this thread is launched with hipExtLaunchKernelGGL bound to them, so
+ * hipEventElapsedTime gives that kernel's execution time as its dispatch records it.  Not
+ * for use under hipGraph capture. */
+int gvl_set_launch_events(void* start, void* stop);
 
 /* ------------------------------------------------------------------------- */
 /* GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulate, fused epilogue.

@@ -1,18 +1,27 @@
 """Per-op CPU fp32 restatements (TEST INFRASTRUCTURE; see oracle/__init__.py).
 
 Explicit math, no fused torch kernels: these are the checkers for the HIP kernels.
+
+FAST_PATHS (off by default; bench.py's cpu_baseline turns it on): attention, LayerNorm,
+GELU and CE call the very torch ops the reference calls (F.scaled_dot_product_attention,
+F.layer_norm, F.gelu, F.cross_entropy) instead of the explicit math, so the timed CPU
+baseline runs at the reference CPU path's speed.  Same results to fp32 rounding (tested).
 """
 from __future__ import annotations
 
 import math
 
 import torch
+import torch.nn.functional as TF
 
 F32 = torch.float32
+FAST_PATHS = False
 
 
 def layernorm(x, w, b, eps=1e-5):
     """nn.LayerNorm (train_gpt2.py:66): biased variance over the last dim."""
+    if FAST_PATHS:
+        return TF.layer_norm(x.to(F32), (x.shape[-1],), w.to(F32), b.to(F32), eps)
     x = x.to(F32)
     mu = x.mean(dim=-1, keepdim=True)
     var = ((x - mu) ** 2).mean(dim=-1, keepdim=True)
@@ -21,11 +30,15 @@ def layernorm(x, w, b, eps=1e-5):
 
 def gelu_tanh(x):
     """nn.GELU(approximate='tanh') (train_gpt2.py:52)."""
+    if FAST_PATHS:
+        return TF.gelu(x, approximate="tanh")
     return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * x ** 3)))
 
 
 def gelu_erf(x):
     """nn.GELU() exact (gpt2_q_former/model.py:128)."""
+    if FAST_PATHS:
+        return TF.gelu(x)
     return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
 
 
@@ -39,6 +52,8 @@ def attention(q, k, v, causal, scale=None):
     """softmax(q k^T * scale [+ causal mask]) v for [B, H, T, 64] tensors
     (F.scaled_dot_product_attention at train_gpt2.py:40, gpt2_cross-att/model.py:55;
     is_causal uses the top-left aligned lower-triangular mask)."""
+    if FAST_PATHS and scale is None:
+        return TF.scaled_dot_product_attention(q.to(F32), k.to(F32), v.to(F32), is_causal=causal)
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     s = (q.to(F32) @ k.to(F32).transpose(-1, -2)) * scale
@@ -64,6 +79,9 @@ def merge_heads(y):
 
 def cross_entropy(logits, targets, ignore_index=-100):
     """F.cross_entropy mean over non-ignored targets (train_gpt2.py:124)."""
+    if FAST_PATHS:
+        return TF.cross_entropy(logits.to(F32).reshape(-1, logits.shape[-1]), targets.reshape(-1),
+                                ignore_index=ignore_index)
     lg = logits.to(F32).reshape(-1, logits.shape[-1])
     t = targets.reshape(-1)
     valid = t != ignore_index

@@ -146,3 +146,27 @@ def test_cross_tiny(golden, meta):
     toks, _ = OM.greedy(lambda s: OM.cross_att_forward(P, s, z[:1], 2, 2)[0],
                         _t(fx["greedy_prompt"]), 16)
     assert toks.tolist() == fx["greedy_tokens"].tolist()
+
+
+def test_fast_paths_match_explicit_math():
+    """oracle.ops.FAST_PATHS (bench.py's timed CPU baseline) computes the same values."""
+    import torch
+    from oracle import ops as O
+    g = torch.Generator().manual_seed(3)
+    q, k, v = (torch.randn(2, 3, 40, 64, generator=g) for _ in range(3))
+    x = torch.randn(5, 7, 96, generator=g)
+    w, b = torch.randn(96, generator=g), torch.randn(96, generator=g)
+    lg = torch.randn(30, 50, generator=g)
+    t = torch.randint(0, 50, (30,), generator=g)
+    t[::4] = -100
+    outs = []
+    for fast in (False, True):
+        O.FAST_PATHS = fast
+        try:
+            outs.append([O.attention(q, k, v, True), O.attention(q, k, v, False),
+                         O.layernorm(x, w, b), O.gelu_tanh(x), O.gelu_erf(x),
+                         O.cross_entropy(lg, t)])
+        finally:
+            O.FAST_PATHS = False
+    for a, b_ in zip(*outs):
+        assert torch.allclose(a, b_, rtol=1e-5, atol=1e-5)
