@@ -202,7 +202,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 6, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 9, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;

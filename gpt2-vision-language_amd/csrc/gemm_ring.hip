@@ -323,6 +323,18 @@ int launch_layout(const GemmP& p, int cfg, hipStream_t s) {
     case 3: return launch_cfg<256, 256, 2, 4, 5, 2, AMN, BMN>(p, s);
     case 4: return launch_pp<4, AMN, BMN>(p, s);
     case 5: return launch_pp<5, AMN, BMN>(p, s);
+    // 192-row tiles: M = 8064 (the caption step, 128 x 63 rows) is exactly 42 of them, so an
+    // N = 768 output is 252 tiles of 192x128 (one round on 256 CUs) instead of 378 of
+    // 128x128 (1.5 rounds) or 96 of 256x256.  K-contiguous A only (the MN image is 128 wide).
+    case 7:
+      if constexpr (!AMN) return launch_cfg<192, 128, 2, 2, 4, 2, AMN, BMN>(p, s);
+      return launch_cfg<128, 128, 2, 2, 4, 1, AMN, BMN>(p, s);
+    case 8:
+      if constexpr (!AMN) return launch_cfg<192, 256, 2, 2, 4, 2, AMN, BMN>(p, s);
+      return launch_cfg<128, 128, 2, 2, 4, 1, AMN, BMN>(p, s);
+    case 9:  // 128x192 (K-contiguous operands only)
+      if constexpr (!AMN && !BMN) return launch_cfg<128, 192, 2, 2, 4, 1, AMN, BMN>(p, s);
+      return launch_cfg<128, 128, 2, 2, 4, 1, AMN, BMN>(p, s);
     default: return launch_cfg<128, 128, 2, 2, 4, 1, AMN, BMN>(p, s);
   }
 }
@@ -338,6 +350,9 @@ const char* gemm_ring_name(int cfg) {
     case 4: return "gemm_pp_kernel<4";
     case 5: return "gemm_pp_kernel<5";
     case 6: return "gemm_ring_kernel<64, 128, 1, 2, 4, 1";
+    case 7: return "gemm_ring_kernel<192, 128, 2, 2, 4, 2";
+    case 8: return "gemm_ring_kernel<192, 256, 2, 2, 4, 2";
+    case 9: return "gemm_ring_kernel<128, 192, 2, 2, 4, 1";
     default: return "gemm_ring_kernel<128, 128, 2, 2, 4, 1";
   }
 }
