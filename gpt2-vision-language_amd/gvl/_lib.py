@@ -94,6 +94,10 @@ SIGNATURES = {
                                 c_f32, c_vp, c_vp]),
     "gvl_adamw_master_dev": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32,
                                        c_f32, c_f32, c_f32, c_vp, c_vp]),
+    "gvl_attn_decode": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                  c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "gvl_sample": (C.c_int, [c_vp, c_i64, c_i32, c_i64, c_i64, c_f32, c_i32, c_f32, c_vp, c_vp,
+                             c_vp]),
     "gvl_colsum_workspace_size": (c_i64, [c_i64, c_i64]),
     "gvl_colsum": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,

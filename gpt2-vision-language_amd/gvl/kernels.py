@@ -281,6 +281,36 @@ def attn_bwd(dout, q, k, v, o, lse, H, causal, dq, dk, dv, scale=None, drop_p=0.
     _lib.check(_L().gvl_attn_bwd(C.byref(d), C.byref(g), _stream()), "gvl_attn_bwd")
 
 
+def attn_decode(q, k, v, H, out=None, scale=None):
+    """One new query per sequence over a KV cache: q [B, *] (head h at cols h*64..), k/v
+    [B, Tk, *] strided views (e.g. slices of a packed [B, Tmax, 3C] cache).  -> o [B, H*64]."""
+    _dev(q, k, v)
+    B, Tk = k.shape[0], k.shape[1]
+    if out is None:
+        out = torch.empty(B, H * 64, dtype=BF16, device=q.device)
+    if scale is None:
+        scale = 1.0 / math.sqrt(64)
+    _lib.check(_L().gvl_attn_decode(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
+                                    k.stride(1), v.data_ptr(), v.stride(0), v.stride(1),
+                                    out.data_ptr(), out.stride(0), B, H, Tk, float(scale),
+                                    _stream()), "gvl_attn_decode")
+    return out
+
+
+def sample(logits2, u, temperature=1.0, top_k=0, top_p=1.0, out=None):
+    """Fused temperature / top-k / top-p draw per row (include/gvl.h gvl_sample); u [rows]
+    fp32 uniforms in [0, 1) on the device.  -> int64 [rows]."""
+    _dev(logits2, u)
+    _rowmajor(logits2, "logits")
+    rows, V = logits2.shape
+    if out is None:
+        out = torch.empty(rows, dtype=torch.int64, device=logits2.device)
+    _lib.check(_L().gvl_sample(logits2.data_ptr(), logits2.stride(0), int(logits2.dtype == F32),
+                               rows, V, float(temperature), int(top_k), float(top_p),
+                               u.data_ptr(), out.data_ptr(), _stream()), "gvl_sample")
+    return out
+
+
 # ---------------------------------------------------------------------- cross entropy
 def cross_entropy(logits2, targets, *, rows_per_group=None, group_stride=0, row_offset=0,
                   mask=None, mask_mode=False, want_grad=True, vocab=None):

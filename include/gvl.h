@@ -226,6 +226,23 @@ int gvl_adamw_master_dev(void* p, float* p_master, const void* g, float* m, floa
                          float weight_decay, const float* grad_scale, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
+/* Incremental decoding (ABI v3).  gvl_attn_decode: one new query per sequence attends all Tk
+ * cached keys (non-causal over the cache = causal for the newest position); q element
+ * (b, h, d) at q + b*q_sb + h*64 + d, key t at k + b*k_sb + t*k_st + h*64 (same for v),
+ * output o + b*o_sb + h*64.  Tk <= 4096.  Replaces the full-sequence recompute of the
+ * reference's decode loops (train_gpt2.py:440-449, gpt2_linear/data.py:111-127) with a KV cache.
+ * gvl_sample: per row, softmax(logits / temperature), keep the top_k largest (0 = all), then
+ * the reference's top-p set (sorted cumulative probability before the token <= top_p, 1 =
+ * all; gpt2_linear/data.py:117-122), and draw with the caller's uniform u[row] in [0, 1) by
+ * inverse CDF in token-index order.  V <= 65536; out int64 [rows]. */
+int gvl_attn_decode(const void* q, int64_t q_sb, const void* k, int64_t k_sb, int64_t k_st,
+                    const void* v, int64_t v_sb, int64_t v_st, void* o, int64_t o_sb, int64_t B,
+                    int64_t H, int64_t Tk, float scale, gvl_stream_t stream);
+int gvl_sample(const void* logits, int64_t ld, int32_t logits_fp32, int64_t rows, int64_t V,
+               float temperature, int32_t top_k, float top_p, const float* u, int64_t* out,
+               gvl_stream_t stream);
+
+/* ------------------------------------------------------------------------- */
 /* Small fused elementwise helpers on the hot path. */
 /* Column sums of a bf16 [rows][cols] matrix (row stride ld) -> bf16 out[cols]
  * (bias gradients); accumulate adds into out. workspace: gvl_colsum_workspace_size. */

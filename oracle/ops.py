@@ -165,3 +165,41 @@ def encode_caption(ids, max_len, eot):
     mask = torch.zeros_like(y, dtype=torch.bool)
     mask[: max(L - 1, 1)] = True
     return x, y, mask
+
+
+def sampling_distribution(logits, temperature=1.0, top_k=0, top_p=1.0):
+    """The filtered next-token distribution of the reference's samplers, float64 numpy:
+    softmax(logits / T); top-k keeps the k largest (train_gpt2.py:444-446); top-p keeps the
+    sorted prefix whose preceding cumulative probability is <= top_p (gpt2_linear/data.py:
+    116-122: cutoff = cumprobs > p shifted right by one), renormalised."""
+    import numpy as np
+    x = np.asarray(logits, dtype=np.float64) / temperature
+    pr = np.exp(x - x.max())
+    pr /= pr.sum()
+    if 0 < top_k < pr.size:  # ties at the k-th value: lowest index first (stable order)
+        order = np.argsort(-pr, kind="stable")
+        keep = np.zeros(pr.size, dtype=bool)
+        keep[order[:top_k]] = True
+        pr = np.where(keep, pr, 0.0)
+        pr /= pr.sum()
+    if top_p < 1.0:
+        order = np.argsort(-pr, kind="stable")
+        cum = np.cumsum(pr[order])
+        cut = cum > top_p
+        cut[1:] = cut[:-1].copy()
+        cut[0] = False
+        keep = np.zeros(pr.size, dtype=bool)
+        keep[order[~cut]] = True
+        pr = np.where(keep, pr, 0.0)
+        pr /= pr.sum()
+    return pr
+
+
+def inverse_cdf_index(dist, u):
+    """Token drawn by uniform u from `dist` walking token indices in order (gvl_sample's
+    draw; same distribution as torch.multinomial over the reference's sorted list)."""
+    import numpy as np
+    cdf = np.cumsum(dist)
+    i = int(np.searchsorted(cdf, u * cdf[-1], side="right"))
+    kept = np.nonzero(dist > 0)[0]
+    return int(min(i, kept[-1]))

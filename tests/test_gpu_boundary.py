@@ -184,3 +184,44 @@ def test_out_of_range_ids_raise(cuda):
     yign[0, :5] = -100  # ignore_index stays legal
     _, loss = model(x, yign)
     assert torch.isfinite(loss)
+
+
+def test_checkpoint_manager_resume_with_arenas(cuda, tmp_path):
+    """gvl.checkpoint round trip of a gvl-AdamW run (fp32 masters + moments in arenas):
+    save at step 2, resume into a fresh model + optimizer, continue == uninterrupted."""
+    from gvl.checkpoint import CheckpointManager
+    from gvl.train import train_step
+    mbs = _batches(cuda, 2, seed=9)
+    loss_fn = lambda m, b: m(b[0], b[1])[1]
+    ref, _ = _tiny_gpt(cuda)
+    ropt = ref.configure_optimizers(0.1, 1e-3, "cuda")
+    a, _ = _tiny_gpt(cuda)
+    aopt = a.configure_optimizers(0.1, 1e-3, "cuda")
+    mgr = CheckpointManager(str(tmp_path), a, aopt, save_every=2)
+    for step in range(3):
+        train_step(ref, ropt, mbs, loss_fn, 1e-3)
+        if step < 2:
+            train_step(a, aopt, mbs, loss_fn, 1e-3)
+            mgr.maybe_save_rolling(step + 1, False, 5.0)
+    b, _ = _tiny_gpt(cuda)
+    bopt = b.configure_optimizers(0.1, 1e-3, "cuda")
+    start = CheckpointManager(str(tmp_path), b, bopt).resume(map_location=cuda)
+    assert start == 3
+    train_step(b, bopt, mbs, loss_fn, 1e-3)
+    for (n, p), q in zip(ref.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
+
+
+def test_shard_loader_device_prefetch(cuda, tmp_path):
+    """gvl.data.DataLoaderLite(device='cuda'): pinned async prefetch returns the same windows
+    as the host path (train_gpt2.py:177-187)."""
+    from gvl.data import DataLoaderLite
+    rng = np.random.default_rng(0)
+    for i, n in enumerate((900, 1300)):
+        np.save(tmp_path / f"fw_train_{i:06d}.npy", rng.integers(0, 50257, n).astype(np.uint16))
+    for rank in range(2):
+        h = DataLoaderLite(2, 32, rank, 2, "train", data_root=str(tmp_path))
+        d = DataLoaderLite(2, 32, rank, 2, "train", data_root=str(tmp_path), device=cuda)
+        for _ in range(25):
+            (hx, hy), (dx, dy) = h.next_batch(), d.next_batch()
+            assert dx.is_cuda and torch.equal(hx, dx.cpu()) and torch.equal(hy, dy.cpu())
