@@ -93,6 +93,7 @@ def run_lm(args, world, rank, dev, timer=None):
         return train_step(model, opt, batches, loss_fn, lr_fn(it), buckets=buckets)
 
     step.graph_args = (model, opt, batches, loss_fn, lr_fn)
+    step.buckets = buckets
     tokens_per_step = B * T * accum * world
     return step, tokens_per_step, dict(workload="gpt2-124m-lm-pretrain", micro_batch=B,
                                        seq_len=T, grad_accum=accum,
@@ -123,9 +124,66 @@ def run_caption(kind, args, world, rank, dev):
         return train_step(model, opt, [(z, x, y, m)], loss_fn, lr_fn(it), buckets=buckets)
 
     step.graph_args = (model, opt, [(z, x, y, m)], loss_fn, lr_fn)
+    step.buckets = buckets
 
     return step, B * world, dict(workload=f"{kind}-caption-step", micro_batch=B, seq_len=31,
                                  grad_accum=1, global_batch=B * world)
+
+
+def run_pixels(args, world, rank, dev, steps, warmup):
+    """BASELINE configs[3]: (B,3,224,224) pixels -> frozen CLIP ViT-L/14 (stock PyTorch-ROCm,
+    bf16) -> fused pool -> linear-bridge caption step (gvl).  The caption step is the graphed
+    train step fed from a static feature buffer; CLIP runs eagerly before it each step."""
+    from gvl.clip import FLOP_PER_IMAGE, CLIPFeatureStage, synthetic_pixels
+    from gvl.train import caption_batch, caption_labels
+    B = args.caption_batch
+    clip = CLIPFeatureStage().to(dev).to(torch.bfloat16)
+    pixels = synthetic_pixels(B, device=dev)
+    model = build_caption("linear", dev)
+    model.train()
+    opt = _quiet(lambda: model.configure_optimizers(0.1, 1e-3, "cuda"))
+    _, x, y, m = caption_batch(B, rank=rank, device=dev)
+    lab = caption_labels(y, m)
+    zbuf = torch.empty(B, 33, 768, dtype=torch.bfloat16, device=dev)
+    zbuf.copy_(clip.features(pixels))
+    loss_fn = lambda mm, b: mm(b[0], b[1], labels=b[2])[1]  # noqa: E731
+    from gvl.optim import get_lr
+    lr_fn = lambda it: get_lr(it, 1e-3, 1e-4, 5, 80)  # noqa: E731
+    if world == 1 and not args.no_graph:
+        from gvl.graph import GraphedStep
+        gs = GraphedStep(model, opt, [(zbuf, x, lab)], loss_fn, lr_fn(0), warmup=2)
+        inner = lambda it: gs(lr_fn(it))  # noqa: E731
+    else:
+        from gvl.train import train_step
+        inner = lambda it: train_step(model, opt, [(zbuf, x, lab)], loss_fn, lr_fn(it))  # noqa: E731
+
+    def step(it):
+        zbuf.copy_(clip.features(pixels))
+        return inner(it)
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        clip.features(pixels)
+    torch.cuda.synchronize()
+    clip_ms = (time.perf_counter() - t0) / steps * 1e3
+    t0 = time.perf_counter()
+    r = None
+    for i in range(steps):
+        r = step(warmup + i)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    val = B / dt
+    return dict(value=round(val, 1), unit="images/s", ms_per_step=round(dt * 1e3, 3),
+                clip_ms_per_batch=round(clip_ms, 3),
+                step_mfma_frac=round(val * (FLOP_PER_IMAGE + CAP_FLOP_PER_IMAGE["linear"]) / 1e12
+                                     / PEAK_BF16_TFLOPS, 4),
+                loss=round(float(r.loss), 5),
+                config=dict(workload="linear-caption-step-pixels", micro_batch=B,
+                            image="3x224x224", clip="ViT-L/14 (stock PyTorch-ROCm, bf16, SDPA)",
+                            pool="fused before the visual projection (gvl)", seq_len=31,
+                            grad_accum=1, global_batch=B))
 
 
 def _quiet(fn):
@@ -136,10 +194,12 @@ def _quiet(fn):
 
 
 def graphed(step, warmup):
-    """Capture the step into one hipGraph (gvl.graph) after `warmup` eager steps."""
+    """Capture the step into hipGraphs (gvl.graph) after `warmup` eager steps: one graph at
+    N=1; at N>1 two graphs around one eager RCCL all-reduce of the grad arena."""
     from gvl.graph import GraphedStep
     model, opt, batches, loss_fn, lr_fn = step.graph_args
-    gs = GraphedStep(model, opt, batches, loss_fn, lr_fn(0), warmup=warmup)
+    gs = GraphedStep(model, opt, batches, loss_fn, lr_fn(0), warmup=warmup,
+                     buckets=getattr(step, "buckets", None))
     return lambda it: gs(lr_fn(it))
 
 
@@ -345,12 +405,15 @@ def main():
     ap.add_argument("--caption-steps", type=int, default=10)
     ap.add_argument("--captions", default="qformer,linear,cross",
                     help="secondary caption-step lines of the default (lm) run")
+    ap.add_argument("--no-pixels", dest="pixels", action="store_false",
+                    help="skip the pixel-input (CLIP ViT-L/14) linear caption line")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU work per cpu_baseline sample (LM; captions get half)")
     ap.add_argument("--no-kernel-pass", action="store_true",
                     help="skip the eager per-GEMM timing pass (profiling runs)")
     ap.add_argument("--no-graph", action="store_true",
-                    help="eager steps (default at N=1: the step is captured into one hipGraph)")
+                    help="eager steps (default: the step is captured into hipGraphs; at N>1 two "
+                         "graphs around the RCCL gradient all-reduce)")
     args = ap.parse_args()
 
     world, rank, dev = setup()
@@ -364,7 +427,7 @@ def main():
     else:
         step, units, cfg = run_caption(args.workload, args, world, rank, dev)
         unit, flop_per_unit = "images/s", CAP_FLOP_PER_IMAGE[args.workload]
-    use_graph = world == 1 and not args.no_graph
+    use_graph = not args.no_graph
     timer = None if args.no_kernel_pass else K.KernelTimer()
     dt, res = timed(step, args.steps, args.warmup, world, timer, graph=use_graph)
     value = units * args.steps / dt
@@ -404,6 +467,9 @@ def main():
             out[f"caption_{kind}"] = line
             del cstep
             torch.cuda.empty_cache()
+    if args.workload == "lm" and not args.no_secondary and args.pixels and world == 1:
+        out["caption_linear_pixels"] = run_pixels(args, world, rank, dev, args.caption_steps, 3)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload, seconds=args.cpu_seconds)
     if rank == 0:

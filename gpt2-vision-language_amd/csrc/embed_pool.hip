@@ -72,7 +72,8 @@ GVL_DEV float ld_in<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 
 template <typename TIn>
 __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ in, void* out,
-                                                       int out_f32, int64_t L, int D, int side) {
+                                                       int out_f32, int64_t L, int D, int side,
+                                                       int normalize) {
   __shared__ float red[POOL_NT / 64];
   const int64_t b = blockIdx.y;
   const int o = blockIdx.x;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
     ss += a * a;
   }
   ss = block_sum<POOL_NT>(ss, red);
-  const float scale = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  const float scale = normalize ? 1.f / fmaxf(sqrtf(ss), 1e-12f) : 1.f;
   const int64_t orow = (b * 33 + o) * (int64_t)D;
 #pragma unroll
   for (int k = 0; k < POOL_MAXD; ++k) {
@@ -114,6 +115,32 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
       const float v = acc[k] * scale;
       if (out_f32) reinterpret_cast<float*>(out)[orow + d] = v;
       else reinterpret_cast<bf16_t*>(out)[orow + d] = f2bf(v);
+    }
+  }
+}
+
+// F.normalize(dim=-1, eps=1e-12) of bf16 / fp32 rows (D <= 1024), one block per row.
+template <typename T>
+__global__ __launch_bounds__(POOL_NT) void l2norm_rows_kernel(const T* __restrict__ in,
+                                                              T* __restrict__ out, int D) {
+  __shared__ float red[POOL_NT / 64];
+  const int64_t r = blockIdx.x;
+  float v[POOL_MAXD];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < POOL_MAXD; ++k) {
+    const int d = threadIdx.x + k * POOL_NT;
+    v[k] = d < D ? ld_in<T>(in + r * D + d) : 0.f;
+    ss += v[k] * v[k];
+  }
+  ss = block_sum<POOL_NT>(ss, red);
+  const float scale = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+  for (int k = 0; k < POOL_MAXD; ++k) {
+    const int d = threadIdx.x + k * POOL_NT;
+    if (d < D) {
+      if constexpr (sizeof(T) == 4) out[r * D + d] = v[k] * scale;
+      else out[r * D + d] = f2bf(v[k] * scale);
     }
   }
 }
@@ -148,8 +175,9 @@ extern "C" int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dw
   return 0;
 }
 
-extern "C" int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
-                             int64_t B, int64_t L, int64_t D, gvl_stream_t stream) {
+extern "C" int gvl_pool_clip_ex(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
+                                int64_t B, int64_t L, int64_t D, int32_t normalize,
+                                gvl_stream_t stream) {
   const int64_t N = L - 1;
   int side = 0;
   while ((int64_t)(side + 1) * (side + 1) <= N) ++side;
@@ -161,10 +189,32 @@ extern "C" int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t
   hipStream_t s = gvl::as_stream(stream);
   if (in_fp32)
     hipLaunchKernelGGL(pool_kernel<float>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
-                       out, (int)out_fp32, L, (int)D, side);
+                       out, (int)out_fp32, L, (int)D, side, (int)normalize);
   else
     hipLaunchKernelGGL(pool_kernel<bf16_t>, grid, dim3(POOL_NT), 0, s,
-                       static_cast<const bf16_t*>(in), out, (int)out_fp32, L, (int)D, side);
+                       static_cast<const bf16_t*>(in), out, (int)out_fp32, L, (int)D, side,
+                       (int)normalize);
   GVL_LAUNCH_CHECK("gvl_pool_clip");
+  return 0;
+}
+
+extern "C" int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
+                             int64_t B, int64_t L, int64_t D, gvl_stream_t stream) {
+  return gvl_pool_clip_ex(in, in_fp32, out, out_fp32, B, L, D, 1, stream);
+}
+
+extern "C" int gvl_l2_normalize_rows(const void* in, void* out, int32_t fp32, int64_t rows,
+                                     int64_t D, gvl_stream_t stream) {
+  GVL_REQUIRE(D > 0 && D <= POOL_NT * POOL_MAXD, "gvl_l2_normalize_rows: D=%lld unsupported",
+              (long long)D);
+  if (rows == 0) return 0;
+  hipStream_t s = gvl::as_stream(stream);
+  if (fp32)
+    hipLaunchKernelGGL(l2norm_rows_kernel<float>, dim3((unsigned)rows), dim3(POOL_NT), 0, s,
+                       static_cast<const float*>(in), static_cast<float*>(out), (int)D);
+  else
+    hipLaunchKernelGGL(l2norm_rows_kernel<bf16_t>, dim3((unsigned)rows), dim3(POOL_NT), 0, s,
+                       static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), (int)D);
+  GVL_LAUNCH_CHECK("gvl_l2_normalize_rows");
   return 0;
 }

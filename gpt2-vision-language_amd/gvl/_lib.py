@@ -86,6 +86,8 @@ SIGNATURES = {
     "gvl_embedding_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64,
                                     c_i64, c_vp]),
     "gvl_pool_clip": (C.c_int, [c_vp, c_i32, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
+    "gvl_pool_clip_ex": (C.c_int, [c_vp, c_i32, c_vp, c_i32, c_i64, c_i64, c_i64, c_i32, c_vp]),
+    "gvl_l2_normalize_rows": (C.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),
     "gvl_grad_norm_workspace_size": (c_i64, [c_i64]),
     "gvl_grad_norm": (C.c_int, [c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
     "gvl_adamw": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32,

@@ -359,8 +359,8 @@ def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset
 
 
 # ------------------------------------------------------------------------------- pool
-def pool_clip(tokens, out_dtype=None):
-    """[B, 1+s*s, D] -> [B, 33, D]: CLS + adaptive-avg (4,8) + L2 normalise."""
+def pool_clip(tokens, out_dtype=None, normalize=True):
+    """[B, 1+s*s, D] -> [B, 33, D]: CLS + adaptive-avg (4,8) (+ L2 normalise)."""
     _dev(tokens)
     t = tokens.contiguous()
     if t.dtype not in (F32, BF16):
@@ -368,8 +368,21 @@ def pool_clip(tokens, out_dtype=None):
     B, L, D = t.shape
     out_dtype = out_dtype or t.dtype
     out = torch.empty(B, 33, D, dtype=out_dtype, device=t.device)
-    _lib.check(_L().gvl_pool_clip(t.data_ptr(), int(t.dtype == F32), out.data_ptr(),
-                                  int(out_dtype == F32), B, L, D, _stream()), "gvl_pool_clip")
+    _lib.check(_L().gvl_pool_clip_ex(t.data_ptr(), int(t.dtype == F32), out.data_ptr(),
+                                     int(out_dtype == F32), B, L, D, int(normalize), _stream()),
+               "gvl_pool_clip")
+    return out
+
+
+def l2_normalize_rows(x, out=None):
+    """F.normalize(x, dim=-1, eps=1e-12) for bf16 / fp32 rows (D <= 1024)."""
+    _dev(x)
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    D = x.shape[-1]
+    _lib.check(_L().gvl_l2_normalize_rows(x.data_ptr(), out.data_ptr(), int(x.dtype == F32),
+                                          x.numel() // D, D, _stream()), "gvl_l2_normalize_rows")
     return out
 
 

@@ -27,13 +27,10 @@ class StepResult:
     norm: torch.Tensor  # 0-dim fp32 on device (pre-clip global grad norm)
 
 
-def train_step(model, optimizer, micro_batches, loss_fn, lr, *, buckets: GradBuckets = None,
-               max_norm: float = 1.0, process_group=None) -> StepResult:
-    """One optimizer step over len(micro_batches) micro-steps.
-
-    loss_fn(model, batch) -> scalar loss tensor.  `buckets` (gvl.dist.GradBuckets) enables
-    the data-parallel gradient all-reduce on the last micro-step.
-    """
+def accumulate(model, optimizer, micro_batches, loss_fn, buckets: GradBuckets = None):
+    """zero_grad, then forward / loss/accum / backward per micro-step (train_gpt2.py:458-469);
+    with `buckets` the gradient all-reduce fires during the last micro-step's backward.
+    Returns the summed micro-step losses (device scalar)."""
     accum = len(micro_batches)
     optimizer.zero_grad()
     loss_accum = None
@@ -46,12 +43,29 @@ def train_step(model, optimizer, micro_batches, loss_fn, lr, *, buckets: GradBuc
         loss.backward()
     if buckets is not None:
         buckets.wait()
-    all_reduce_mean_(loss_accum, process_group)
+    return loss_accum
+
+
+def finish(optimizer, lr, max_norm: float = 1.0):
+    """clip_grad_norm_ (device-side coefficient) -> lr -> AdamW (train_gpt2.py:472-476)."""
     norm = clip_grad_norm_(optimizer, max_norm)
     if lr is not None:  # None: keep the groups' lr (a captured step stages it per replay)
         for g in optimizer.param_groups:
             g["lr"] = lr
     optimizer.step()
+    return norm
+
+
+def train_step(model, optimizer, micro_batches, loss_fn, lr, *, buckets: GradBuckets = None,
+               max_norm: float = 1.0, process_group=None) -> StepResult:
+    """One optimizer step over len(micro_batches) micro-steps.
+
+    loss_fn(model, batch) -> scalar loss tensor.  `buckets` (gvl.dist.GradBuckets) enables
+    the data-parallel gradient all-reduce on the last micro-step.
+    """
+    loss_accum = accumulate(model, optimizer, micro_batches, loss_fn, buckets)
+    all_reduce_mean_(loss_accum, process_group)
+    norm = finish(optimizer, lr, max_norm)
     return StepResult(loss_accum, norm)
 
 

@@ -194,6 +194,14 @@ int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc, flo
  * Replaces pool_clip_197_to_33_avg_with_cls, gpt2_linear/model.py:240-254. */
 int gvl_pool_clip(const void* in, int32_t in_fp32, void* out, int32_t out_fp32,
                   int64_t B, int64_t L, int64_t D, gvl_stream_t stream);
+/* As gvl_pool_clip with the L2 normalisation optional (ABI v3): the pixel-input path pools
+ * CLIP's layer-normed hidden states BEFORE the (linear, bias-free) visual projection — the
+ * average commutes with it — so the projection runs on 33 tokens instead of 257, then
+ * normalises with gvl_l2_normalize_rows (F.normalize(dim=-1, eps=1e-12), D <= 1024). */
+int gvl_pool_clip_ex(const void* in, int32_t in_fp32, void* out, int32_t out_fp32, int64_t B,
+                     int64_t L, int64_t D, int32_t normalize, gvl_stream_t stream);
+int gvl_l2_normalize_rows(const void* in, void* out, int32_t fp32, int64_t rows, int64_t D,
+                          gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Optimizer path over flat bf16 arenas (params / grads / exp_avg / exp_avg_sq).

@@ -104,3 +104,103 @@ def test_gloo_two_ranks_match_single_process():
     assert float(loss_ref) == pytest.approx(l0, rel=1e-6)
     for a, b in zip(m.parameters(), p0):
         assert torch.allclose(a.detach(), b, atol=1e-6), "DP step != single-process step"
+
+
+class _FusedLinear(torch.autograd.Function):
+    """CPU stand-in for a gvl fused unit: the weight gradient is accumulated IN PLACE into the
+    arena view (.grad) and announced through gvl.functional's grad-ready hook, bypassing
+    AccumulateGrad — exactly how GPTBlockFn & co. feed gvl.dist.GradBuckets."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from gvl import functional as F
+        x, w = ctx.saved_tensors
+        w.grad.add_(dy.t() @ x)
+        F._ready(w)
+        return dy @ w, None
+
+
+class _Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = torch.nn.Linear(16, 64)
+        self.w = torch.nn.Parameter(torch.randn(64, 64) * 0.1)  # the fused-sink parameter
+        self.b = torch.nn.Linear(64, 4)
+
+    def forward(self, x):
+        h = torch.nn.functional.gelu(self.a(x))
+        h = torch.nn.functional.gelu(_FusedLinear.apply(h, self.w))
+        return self.b(h)
+
+
+def _worker_accum(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gvl.dist as D
+    from gvl.train import train_step
+    calls = []
+    real = D._avg
+
+    def counting(t, pg, async_op):
+        calls.append((len(seen), t.numel()))
+        return real(t, pg, async_op)
+    D._avg = counting
+    seen = []
+    m = _Net()
+    opt = ArenaSGD(m.parameters(), lr=0.1)
+    bk = D.GradBuckets(opt, bucket_mb=1024 * 4 / (1024 * 1024))
+    x, y = _data(rank, 16)
+    mbs = [(x[i * 4:(i + 1) * 4], y[i * 4:(i + 1) * 4]) for i in range(4)]
+
+    def loss_fn(mm, b):
+        seen.append(bk.sync)
+        return ((mm(b[0]) - b[1]) ** 2).mean()
+    res = train_step(m, opt, mbs, loss_fn, lr=0.1, buckets=bk, max_norm=1e9)
+    q.put((rank, len(bk.buckets), seen, calls, float(res.loss),
+           [p.detach().numpy().copy() for p in m.parameters()]))
+    bk.remove()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_gloo_buckets_with_fused_sinks_and_sync_toggle():
+    """GradBuckets over the arena with a fused in-place-accumulating parameter, 4 micro-steps:
+    sync is off for micro-steps 0-2 and on for 3 (train_gpt2.py:468), every bucket is reduced
+    exactly once and only during the last micro-step, and the result equals one process over
+    the concatenated batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_accum, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=150) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, nb, seen, calls, loss, params in out:
+        assert len(seen) == 4  # (sync is toggled after each forward, before its backward)
+        assert nb >= 2 and len(calls) == nb + 1, (nb, calls)  # every bucket once + the loss
+        assert all(step == 4 for step, _ in calls), "a bucket fired before the sync micro-step"
+    assert out[0][4] == pytest.approx(out[1][4])
+    m = _Net()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    chunks = []
+    for r in range(2):
+        x, y = _data(r, 16)
+        chunks += [(x[i * 4:(i + 1) * 4], y[i * 4:(i + 1) * 4]) for i in range(4)]
+    opt.zero_grad()
+    loss_ref = sum(((m(a) - b) ** 2).mean() for a, b in chunks) / 8
+    # _FusedLinear needs an existing .grad to accumulate into (the arena view in gvl)
+    m.w.grad = torch.zeros_like(m.w)
+    loss_ref.backward()
+    opt.step()
+    assert float(loss_ref) == pytest.approx(out[0][4], rel=1e-6)
+    for a, b in zip(m.parameters(), out[0][5]):
+        assert torch.allclose(a.detach(), torch.from_numpy(b), atol=1e-6)

@@ -151,3 +151,19 @@ def test_topk_sampling_reproducible(cuda):
     toks, lg = outs[0]
     top = lg.topk(50, dim=-1).indices
     assert (top == toks.unsqueeze(-1)).any(-1).all()
+
+
+def test_clip_fused_pool_equals_unfused(cuda):
+    """Pixel path (BASELINE configs[3]): pooling CLIP's layer-normed hidden states before the
+    bias-free projection (gvl) == pool_clip_197_to_33_avg_with_cls of the projected tokens
+    (gpt2_linear/model.py:240-254), up to bf16 rounding."""
+    from gvl.clip import CLIPFeatureStage, synthetic_pixels
+    clip = CLIPFeatureStage().to(cuda).to(BF)
+    px = synthetic_pixels(2, device=cuda)
+    a = clip.features(px, fused=True).float()
+    b = clip.features(px, fused=False).float()
+    assert tuple(a.shape) == (2, 33, 768)
+    err = (a - b).abs().max().item() / b.abs().max().item()
+    norms = a.norm(dim=-1)
+    print(f"fused vs unfused pool: rel err {err:.2e}; row norms {norms.min().item():.4f}..{norms.max().item():.4f}")
+    assert err < 3e-2 and torch.allclose(norms, torch.ones_like(norms), atol=1e-2)
