@@ -148,8 +148,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
   gemm_epilogue<4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-// GVL_GEMM_IMPL=regstage|lds|ring|pp picks the kernel family (0|1|2|3, default 3: the
-// persistent ping-pong kernel where it fills the chip, else the 128x128 ring);
+// GVL_GEMM_IMPL=regstage|lds|ring|pp|8p picks the kernel family (0|1|2|3|4, default 3: the
+// persistent ping-pong kernel where it fills the chip, else the 128x128 ring; 4: the
+// quadrant-phase kernel of gemm_8p.hip where K % 64 == 0, else as 3);
 // GVL_GEMM_CFG forces a tile config of that family.
 struct GemmEnv {
   int impl = 3, cfg = -1, group = 8;
@@ -161,6 +162,7 @@ struct GemmEnv {
     if (s && s[0] == 'l') impl = 1;
     if (s && s[0] == 'r' && s[1] == 'i') impl = 2;
     if (s && s[0] == 'p') impl = 3;
+    if (s && s[0] == '8') impl = 4;
     const char* c = getenv("GVL_GEMM_CFG");
     if (c) cfg = atoi(c);
   }
@@ -202,7 +204,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 9, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 9, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -211,10 +213,15 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
-  if (env().impl == 3 && gvl::gemm_ring_ok(d)) {
+  if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     GemmP p;
     fill_params(d, p);
-    if (env().cfg >= 0) {
+    GemmP q = p;
+    if (env().impl == 4 && env().cfg < 0 && gvl::gemm_8p_plan(q, false)) {
+      const char* epi[9] = {"0", "1", "2", "3", "4", "5", "6", "7", "8"};
+      snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
+               epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
+    } else if (env().cfg >= 0) {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg), tf[d->a_mn != 0],
                tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
@@ -261,9 +268,10 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GemmP p;
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
-  if (env().impl == 3 && gvl::gemm_ring_ok(d)) {
+  if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     if (env().cfg >= 0) {
       gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg, s);
+    } else if (env().impl == 4 && gvl::gemm_8p_try(p, d->a_mn, d->b_mn, false, s)) {
     } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
       gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn), s);
     }

@@ -343,7 +343,9 @@ int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced, int a_mn);
 const char* gemm_pp2_name(int cfg);
 int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
 int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels
-bool gemm_pp3_plan(GemmP& p, bool force);
+bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
-int gemm_pp3_splits(int64_t M, int64_t N, int64_t K);
+int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
+bool gemm_8p_plan(GemmP& p, bool force);
+bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 }  // namespace gvl

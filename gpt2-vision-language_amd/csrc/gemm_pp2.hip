@@ -382,14 +382,14 @@ int gemm_epi_kind(const GemmP& p) {
 // 256x256 tile's 32-deep K-step, T(s) = rounds(tiles*s) * (K/32s + 6) + slab round trip
 // (s fp32 partials written + read, at ~6 TB/s, ~1.1 PF/s of MFMA per 256 CUs); slices must
 // be equal and at least 16 K-steps deep.
-int gemm_pp3_splits(int64_t M, int64_t N, int64_t K) {
+int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int cus = num_cus();
   const double step_s = 2.0 * 256 * 256 * 32 / (1.1e15 / cus);
   double best = 1e30;
   int best_s = 1;
   for (int s = 1; s <= 16; ++s) {
-    if (K % (32 * s) != 0 || (s > 1 && K / s < 512)) continue;
+    if (K % ((int64_t)gran * s) != 0 || (s > 1 && K / s < 512)) continue;
     const int64_t rounds = (tiles * s + cus - 1) / cus;
     double t = (double)rounds * ((double)K / (32.0 * s) + 6.0);
     if (s > 1) t += (double)s * M * N * 8.0 / 6e12 / step_s;
@@ -411,14 +411,14 @@ static int64_t pp3_min_items() {
   return v;
 }
 
-bool gemm_pp3_plan(GemmP& p, bool force) {
+bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
   p.tiles_m = (int)((p.M + 255) / 256);
   p.tiles_n = (int)((p.N + 255) / 256);
   p.splits = 1;
   if (p.ws != nullptr) {
-    const int sp = gemm_pp3_splits(p.M, p.N, p.K);
+    const int sp = gemm_pp3_splits(p.M, p.N, p.K, gran);
     if (sp > 1 && (int64_t)sp * p.M * p.N * 4 <= p.ws_bytes) p.splits = sp;
   }
   p.kper = p.K / p.splits;

@@ -1,9 +1,12 @@
 """Per-kernel HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md § HBM):
-FETCH_SIZE counts half the bytes of wide coalesced streaming reads (every libgvl GEMM operand
-moves by 16-B-per-lane buffer_load ... lds), so it is doubled; WRITE_SIZE is exact for the
-16-B-per-lane stores the GEMM epilogues issue.
+FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction, calibrated on known-byte kernels
+(tools/pmc_calib.sh -> profiles/r2/pmc_calibration.json): FETCH_SIZE counts half the bytes of
+16-B-per-lane streaming reads — expected/counter = 1.995 for the CE kernel's register loads and
+1.90 for a GEMM whose A operand (512 MiB, read once) moves by buffer_load ... lds (the 5 % gap
+is B re-fetched per XCD) — so it is doubled; WRITE_SIZE is exact for 16-B stores (0.998-1.000).
+Kernels with narrower loads (LayerNorm backward's 8-B accesses) are not calibrated: their
+traffic is an estimate.
 usage: python tools/pmc_traffic.py DIR   (DIR holds {lm,qf}_{FETCH_SIZE,WRITE_SIZE}/**.csv)"""
 import csv
 import glob

@@ -1,14 +1,14 @@
 #!/bin/bash
-# HBM traffic of the bench's kernels from PMC counters (MI355X_MICROARCH.md § HBM): one
+# HBM traffic of the bench's kernels from PMC counters (calibration: profiles/r2/pmc_calibration.md): one
 # rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), kernel-trace
 # only, eager step (graph replays are not attributed per dispatch), each pass time-limited.
 # Then tools/pmc_traffic.py turns them into per-launch bytes -> gpurun_out/pmc_traffic_$TAG.json.
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; TAG=${1:-x}
 OUT=gpurun_out/pmc_traffic_$TAG; mkdir -p $OUT
-# a deep queue of eager dispatches under --pmc aborted once with HSA_STATUS_ERROR_INVALID_PACKET_FORMAT
-# (profiler packet injection); serialising dispatches keeps the queue shallow
-export AMD_SERIALIZE_KERNEL=3
+# Round 1 ran these passes with AMD_SERIALIZE_KERNEL=3 after one HSA_STATUS_ERROR_INVALID_PACKET_FORMAT
+# abort; the same eager LM pass without it completed in round 2 (tools/pmc_calib.sh,
+# profiles/r2/pmc_calibration.md), so the passes run unserialised.
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/lm_$c -o run -- \
     python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $OUT/lm_$c.log 2>&1 || exit $?
