@@ -428,7 +428,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
 // dK/dV: block = (64*G-key tile, head, batch), waves own G groups of 16 keys; loop over
 // 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
+__global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int KB = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
@@ -626,6 +626,16 @@ int fill(const gvl_attn_desc* d, AttnP& p) {
 // the short caption sequences (31-64 rows) keep 64-row blocks.
 int pick_groups(int64_t T) { return T > 64 ? 2 : 1; }
 
+// dK/dV key groups per wave: GVL_DKDV_G=2 runs 32 keys per wave (one wave per SIMD, the
+// accumulators need > 256 registers) for Tk > 64; default 1.
+int dkdv_groups(int64_t Tk) {
+  static const int g = [] {
+    const char* e = getenv("GVL_DKDV_G");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return (g == 2 && Tk > 64) ? 2 : 1;
+}
+
 // Block count of the 1-D heavy-first grid (see tile_of_block); fill() bounds it.
 unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntile * d->H * d->B); }
 
@@ -687,9 +697,15 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
   // dK/dV keeps one 16-key group per wave: two groups need >256 VGPRs (dK and dV
   // accumulators for 32 keys x 64 dims) and spill to scratch.
-  dim3 gk(grid_1d(d, (d->Tk + 63) / 64));
-  if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), gk, dim3(NT), 0, s, p, g);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), gk, dim3(NT), 0, s, p, g);
+  const int Gk = dkdv_groups(d->Tk);
+  dim3 gk(grid_1d(d, (d->Tk + 64 * Gk - 1) / (64 * Gk)));
+  if (Gk == 2) {
+    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), gk, dim3(NT), 0, s, p, g);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), gk, dim3(NT), 0, s, p, g);
+  } else {
+    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), gk, dim3(NT), 0, s, p, g);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), gk, dim3(NT), 0, s, p, g);
+  }
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");
   return 0;
 }

@@ -386,8 +386,9 @@ def test_attention_noncausal(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False)
 
 
-def test_attention_dropout_exact_mask(cuda):
-    _attn_case(cuda, 2, 2, 32, 33, False, packed=False, drop_p=0.1, seed=4242)
+@pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130)])
+def test_attention_dropout_exact_mask(cuda, Tq, Tk):
+    _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False, drop_p=0.1, seed=4242)
 
 
 def test_attention_matches_reference_fixture(cuda, golden):
