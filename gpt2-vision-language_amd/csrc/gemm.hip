@@ -194,6 +194,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
   p.splits = 1;
+  p.bn = 256;
   p.kper = d->k;
   p.group = env().group;
   p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
@@ -226,8 +227,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
                tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
       const char* epi[9] = {"0", "1", "2", "3", "4", "5", "6", "7", "8"};
-      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
-               epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)]);
+      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
+               epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)], p.bn);
     } else {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn)),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);

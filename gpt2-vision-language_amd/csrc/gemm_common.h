@@ -22,6 +22,7 @@ struct GemmP {
   float drop_scale;
   uint32_t drop_thresh;
   int tiles_m, tiles_n;
+  int bn;     // output tile width of the persistent kernel (256 or 192; gemm_pp3_plan)
   int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
@@ -255,10 +256,10 @@ static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a,
 // v_permlane16_swap_b32 (lanes l <-> l^16 across the pair) leave every lane 8 consecutive
 // columns: quad q stores cols 16 (j + (q & 1)) + 8 (q >> 1) .. + 7, so one store
 // instruction writes 16 rows x 64 B instead of 16 rows x 32 B.
+// Odd FN: the last fragment is stored unpaired (8-B stores).
 template <int FM, int FN, int EPI = EPI_GEN>
 GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
                              int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI>& pre) {
-  static_assert(FN % 2 == 0, "fragment pairs");
   float gatev = 1.f;
   if constexpr (EPI == EPI_GEN) gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
   const bool plain = EPI == EPI_PLAIN ||
@@ -271,7 +272,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
     const bool mok = m < p.M;
     if (EpiKind<EPI>::AUX && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i);
 #pragma unroll
-    for (int j = 0; j < FN; j += 2) {
+    for (int j = 0; j + 1 < FN; j += 2) {
       const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
       uint32_t x0, y0, x1, y1;  // packed bf16 pairs: frag j (x0: cols 0-1, y0: 2-3), frag j+1
       if (plain) {
@@ -308,6 +309,28 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
       if (mok && n < p.N)
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
             make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    }
+    if constexpr (FN % 2 == 1) {
+      constexpr int j = FN - 1;
+      const int64_t n0 = nw0 + j * 16 + 4 * q;
+      uint32_t x0, y0;
+      if (plain) {
+        x0 = pack2(acc[i][j][0] * alpha, acc[i][j][1] * alpha);
+        y0 = pack2(acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+      } else {
+        float v0[4] = {0.f, 0.f, 0.f, 0.f}, h0[4] = {0.f, 0.f, 0.f, 0.f};
+        using KD = EpiKind<EPI>;
+        const uint2 b0 = KD::BIAS ? pre.b[KD::BIAS ? j : 0] : make_uint2(0, 0);
+        constexpr int XH = EpiPre<FM, FN, EPI>::XH;
+        const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
+        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0);
+        x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
+        if (KD::ACT && p.pre_out && mok && n0 < p.N)
+          *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n0) =
+              make_uint2(pack2(h0[0], h0[1]), pack2(h0[2], h0[3]));
+      }
+      if (mok && n0 < p.N)
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n0) = make_uint2(x0, y0);
     }
   }
 }

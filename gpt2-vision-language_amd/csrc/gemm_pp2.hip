@@ -160,14 +160,29 @@ int launch_pp2(const GemmP& p0, hipStream_t s) {
 // Split-K: work item w = (tile w / splits, K-slice w % splits), every slice kper deep (the
 // host only splits when K divides evenly); slices store fp32 partials, gemm_splitk_reduce
 // applies the epilogue.  KC = 1, bf16 output.
-template <int NS, bool AMN, bool BMN, int EPI>
+template <int BN, bool BMN>
+struct SlabB {
+  using type = Step<256, BMN, 8>;
+};
+template <bool BMN>
+struct SlabB<192, BMN> {
+  using type = Step192<BMN>;
+};
+
+// BN = 192 (FN = 3 fragments of 16 columns per wave): for N = 768 / 2304 outputs the 256-wide
+// tiles leave CUs idle in the last round (M = 16384, N = 768: 192 tiles on 256 CUs; 192-wide:
+// 256 tiles).  Its B slab is 12 DMA pieces: waves 0-3 (group 0) issue 2, waves 4-7 one, so
+// the counted waits use a per-group pieces-per-step count.
+template <int NS, bool AMN, bool BMN, int EPI, int BN = 256>
 __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
-  constexpr int BM = 256, BN = 256, NW = 8, FM = 8, FN = 4;
+  constexpr int BM = 256, NW = 8, FM = 8, FN = BN / 64;
   static_assert(NS >= 3 && NS <= 5, "ring geometry");
+  static_assert(BN == 256 || BN == 192, "tile width");
   using SA = Step<BM, AMN, NW>;
-  using SB = Step<BN, BMN, NW>;
+  using SB = typename SlabB<BN, BMN>::type;
   constexpr int SLOT = SA::BYTES + SB::BYTES;
-  constexpr int IPW = (SA::NINSTR + SB::NINSTR) / NW;
+  constexpr int IPW0 = SA::PER + SB::PER;                       // group 0 waves
+  constexpr int IPW1 = SA::PER + (BN == 256 ? SB::PER : 1);     // group 1 waves
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -231,12 +246,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int arow = g * 128, bcol = wc * 64;
+  const int arow = g * 128, bcol = wc * (BN / 4);
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i) GVL_PP3_ISSUE(i);
   {
-    const int r = nsteps - 1;
-    wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+    const int r = nsteps - 1, n = r < 0 ? 0 : (r < NS - 2 ? r : NS - 2);
+    if (g == 0) wait_vm_steps<IPW0, NS - 2>(n);
+    else wait_vm_steps<IPW1, NS - 2>(n);
   }
   barrier_lds();
   if (g == 1) __builtin_amdgcn_s_barrier();
@@ -280,7 +296,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     GVL_PP3_ISSUE(c + NS - 1);
     {
       const int r = nsteps - (c + 2);  // steps issued but not needed by step c+1
-      if (g == 1) wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+      if (g == 1) wait_vm_steps<IPW1, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
     }
     barrier_lds();
     // ---- C(c)
@@ -293,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     if (++cu_k == nks) cu_k = 0;
     {
       const int r = nsteps - (c + 2);
-      if (g == 0) wait_vm_steps<IPW, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+      if (g == 0) wait_vm_steps<IPW0, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
     }
     barrier_lds();
   }
@@ -303,11 +319,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
 #undef GVL_PP3_EPILOGUE
 }
 
-template <int NS, bool AMN, bool BMN, int EPI>
-int launch_pp3(const GemmP& p0, hipStream_t s) {
+template <int NS, bool AMN, bool BMN, int EPI, int BN>
+int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
   GemmP p = p0;  // tiles_m/n, splits, kper set by gemm_pp3_try
-  constexpr int lds = NS * 512 * KS * 2;
-  auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI>;
+  constexpr int lds = NS * (256 + BN) * KS * 2;
+  auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI, BN>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -318,6 +334,12 @@ int launch_pp3(const GemmP& p0, hipStream_t s) {
   gvl::launch_timed(kern, dim3(grid), dim3(512), lds, s, p);
   if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
+}
+
+template <int NS, bool AMN, bool BMN, int EPI>
+int launch_pp3(const GemmP& p, hipStream_t s) {
+  return p.bn == 192 ? launch_pp3_bn<NS, AMN, BMN, EPI, 192>(p, s)
+                     : launch_pp3_bn<NS, AMN, BMN, EPI, 256>(p, s);
 }
 
 template <int NS, bool AMN, bool BMN>
@@ -411,6 +433,24 @@ static int64_t pp3_min_items() {
   return v;
 }
 
+// Output tile width: 192 when its tiles fill the last round of CUs better than 256-wide ones
+// (per-tile efficiency of the narrower tile counted at 0.9); GVL_PP3_BN=256|192 forces one.
+static int pp3_tile_width(int64_t M, int64_t N) {
+  static const int forced = [] {
+    const char* e = getenv("GVL_PP3_BN");
+    return e ? atoi(e) : 0;
+  }();
+  if (N % 64 != 0 || N < 384) return 256;
+  if (forced == 256 || forced == 192) return forced;
+  const int64_t cus = num_cus(), tm = (M + 255) / 256;
+  auto fill = [&](int64_t tiles) {
+    const int64_t rounds = (tiles + cus - 1) / cus;
+    return (double)tiles / (double)(rounds * cus);
+  };
+  const double e256 = fill(tm * ((N + 255) / 256)), e192 = 0.9 * fill(tm * ((N + 191) / 192));
+  return e192 > e256 ? 192 : 256;
+}
+
 bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
@@ -423,6 +463,9 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   }
   p.kper = p.K / p.splits;
   if (p.splits == 1 && gemm_epi_kind(p) == EPI_GEN) return false;
+  p.bn = 256;
+  if (p.splits == 1 && gran == KS) p.bn = pp3_tile_width(p.M, p.N);
+  if (p.bn != 256) p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
   if (force) return true;
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
   // split-K slabs only pay off for really few tiles (dW, the caption lm_head dX); with

@@ -96,6 +96,75 @@ struct Step {
   }
 };
 
+// 192-wide operand slab of a 32-deep K-step for 8 waves (gemm_pp3_kernel with BN = 192):
+// 12 DMA pieces, so waves 0-3 issue two and waves 4-7 one (piece j = wave + 8 t, j < 12).
+//  * K-contiguous: [192 rows][32] 64-B rows, the Step image;
+//  * MN-contiguous: cols 0-127 as the Step [32][128] half (256-B rows, fT swizzle), cols
+//    128-191 as [32][64] 128-B rows at +8 KiB, chunk c of k-row kr at c ^ f2(kr) (conflict-free
+//    ds_read_b64_tr_b16 lane groups for the fragment pattern below).
+GVL_DEV int f2(int k) { return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1; }  // 128-B rows
+
+template <bool MN>
+struct Step192 {
+  static constexpr int R = 192, NWV = 8;
+  static constexpr int BYTES = R * KS * 2;
+  static constexpr int NINSTR = BYTES / 1024;  // 12
+  static constexpr int PER = 2;                // pieces of waves 0-3 (waves 4-7: 1)
+  GVL_DEV static int64_t elem(int64_t ld, int64_t r0, int64_t k0, int j, int lane) {
+    if (!MN) {
+      const int row = 16 * j + (lane >> 2);
+      return (r0 + row) * ld + k0 + ((lane & 3) ^ f64b(row)) * 8;
+    }
+    if (j < 8) {
+      const int kr = 4 * j + (lane >> 4);
+      return (k0 + kr) * ld + r0 + ((lane & 15) ^ fT(kr)) * 8;
+    }
+    const int kr = 8 * (j - 8) + (lane >> 3);
+    return (k0 + kr) * ld + r0 + 128 + ((lane & 7) ^ f2(kr)) * 8;
+  }
+  GVL_DEV static void base_offsets(int64_t ld, int64_t r0, int64_t k0, int wave, int lane,
+                                   int (&off)[PER]) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int j = t * NWV + wave;
+      off[t] = j < NINSTR ? (int)(elem(ld, r0, k0, j, lane) * 2) : 0;
+    }
+  }
+  GVL_DEV static int step_bytes(int64_t ld) { return MN ? (int)(KS * ld * 2) : KS * 2; }
+  GVL_DEV static void issue_at(__amdgpu_buffer_rsrc_t rs, const int (&off)[PER], int kbytes,
+                               char* lds, int wave) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int j = t * NWV + wave;
+      if (j < NINSTR)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + j * 1024), 16, off[t],
+                                                 kbytes, 0, 0);
+    }
+  }
+  GVL_DEV static short8_t frag(const char* lds, int c0, int lane) {
+    if (!MN) {
+      const int row = c0 + (lane & 15), ch = lane >> 4;
+      return *reinterpret_cast<const short8_t*>(lds + row * 64 + ((ch ^ f64b(row)) << 4));
+    }
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int kr = 8 * G + q;
+    short8_t r;
+    if (c0 < 128) {
+      const int ch = (c0 >> 3) + (p >> 1);
+      const int off1 = kr * 256 + ((ch ^ fT(kr)) << 4) + (p & 1) * 8;
+      r.lo = lds_read_tr(lds + off1);
+      r.hi = lds_read_tr(lds + off1 + 4 * 256);
+    } else {
+      const int ch = ((c0 - 128) >> 3) + (p >> 1);
+      const char* base = lds + 8192;
+      const int off1 = kr * 128 + ((ch ^ f2(kr)) << 4) + (p & 1) * 8;
+      r.lo = lds_read_tr(base + off1);
+      r.hi = lds_read_tr(base + off1 + 4 * 128);
+    }
+    return r;
+  }
+};
+
 // s_waitcnt vmcnt(n * PER) for a runtime n in [0, MAXN]: the count must be an immediate.
 template <int PER, int MAXN>
 GVL_DEV void wait_vm_steps(int n) {

@@ -159,6 +159,44 @@ def test_gemm_quadrant_phase_kernel(cuda, a_mn, b_mn, epi, M, N, K):
         assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "res_inplace", "bias_act", "dact"])
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (12000, 1536, 320), (16384, 2304, 32)])
+def test_gemm_tile192(cuda, a_mn, b_mn, epi, M, N, K):
+    """192-wide output tiles of the persistent kernel (picked when they fill the last round of
+    CUs better: 16384 x 768 -> 256 tiles instead of 192): every layout incl. the split
+    [32][128] + [32][64] MN-contiguous B image, odd fragment count in the epilogue (3 x 16
+    columns per wave), ragged M, a single K-step."""
+    K_ = _k()
+    torch.manual_seed(M + N + K + len(epi) + 5 * a_mn + 11 * b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.1).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    assert _kernel_name(A, B, a_mn, b_mn, M, N, K).endswith(", 192>")
+    h = a.float() @ b.float()
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    kw, ref = {}, h
+    if epi == "bias_res":
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "res_inplace":
+        acc = res.to(cuda)
+        kw, ref = dict(residual=acc, out=acc), h + res.float()
+    elif epi == "bias_act":
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=1, pre_out=pre), O.gelu_tanh(h + bias.float())
+    elif epi == "dact":
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_tanh(hx).sum().backward()
+        kw, ref = dict(dact=1, pre_in=hpre.to(cuda)), h * hx.grad
+    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    if epi == "bias_act":
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
                                              (0, 0, 384, 256, 6144)])
 @pytest.mark.parametrize("impl", [3, 2, 4])
