@@ -107,6 +107,21 @@ GVL_DEV float dgelu_tanh(float x) {
   const float s = gelu_tanh_sig(x, x2);
   return fmaf(x * s * (1.f - s), fmaf(D, x2, C), s);
 }
+// GELU and its derivative at once (one sigmoid / one erf), for the forward epilogues that
+// store gelu'(x) for the backward instead of x.
+GVL_DEV void gelu_dgelu_tanh(float x, float& g, float& dg) {
+  constexpr float C = 2.f * 0.7978845608028654f, D = 3.f * 0.044715f * C;
+  const float x2 = x * x;
+  const float s = gelu_tanh_sig(x, x2);
+  g = x * s;
+  dg = fmaf(x * s * (1.f - s), fmaf(D, x2, C), s);
+}
+GVL_DEV float fast_erf(float x);
+GVL_DEV void gelu_dgelu_erf(float x, float& g, float& dg) {
+  const float cdf2 = 1.f + fast_erf(x * 0.7071067811865476f);  // 2 Phi(x)
+  g = 0.5f * x * cdf2;
+  dg = fmaf(x * 0.3989422804014327f, __builtin_amdgcn_exp2f(-0.7213475204444817f * x * x), 0.5f * cdf2);
+}
 GVL_DEV float fast_erf(float x) {
   const float a = fabsf(x);
   const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * a);

@@ -219,14 +219,14 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     fill_params(d, p);
     GemmP q = p;
     if (env().impl == 4 && env().cfg < 0 && gvl::gemm_8p_plan(q, false)) {
-      const char* epi[9] = {"0", "1", "2", "3", "4", "5", "6", "7", "8"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
       snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
     } else if (env().cfg >= 0) {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg), tf[d->a_mn != 0],
                tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
-      const char* epi[9] = {"0", "1", "2", "3", "4", "5", "6", "7", "8"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[p.splits > 1 ? 0 : gvl::gemm_epi_kind(p)], p.bn);
     } else {
@@ -262,7 +262,7 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
               "gvl_gemm: leading dims must be multiples of 8 (lda, ldb) / 4 (ldc)");
   GVL_REQUIRE(gvl::aligned16(d->a) && gvl::aligned16(d->b) && gvl::aligned8(d->c),
               "gvl_gemm: operands must be 16-byte aligned");
-  GVL_REQUIRE(d->act >= 0 && d->act <= 2 && d->dact >= 0 && d->dact <= 2, "gvl_gemm: bad act");
+  GVL_REQUIRE(d->act >= 0 && d->act <= 4 && d->dact >= 0 && d->dact <= 3, "gvl_gemm: bad act");
   GVL_REQUIRE(!d->dact || (d->pre_in && d->ldp % 4 == 0), "gvl_gemm: dact needs pre_in");
   GVL_REQUIRE(!d->residual || d->ldr % 4 == 0, "gvl_gemm: ldr must be a multiple of 4");
   GVL_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "gvl_gemm: drop_p out of range");

@@ -310,6 +310,9 @@ void launch_8p_epi(const GemmP& p, hipStream_t s) {
     case EPI_RES: return launch_8p<AMN, BMN, EPI_RES>(p, s);
     case EPI_BIAS_ACT_ERF: return launch_8p<AMN, BMN, EPI_BIAS_ACT_ERF>(p, s);
     case EPI_DACT_ERF: return launch_8p<AMN, BMN, EPI_DACT_ERF>(p, s);
+    case EPI_BIAS_ACT_D: return launch_8p<AMN, BMN, EPI_BIAS_ACT_D>(p, s);
+    case EPI_BIAS_ACT_ERF_D: return launch_8p<AMN, BMN, EPI_BIAS_ACT_ERF_D>(p, s);
+    case EPI_MUL: return launch_8p<AMN, BMN, EPI_MUL>(p, s);
     default: return;  // unreachable (gemm_8p_plan)
   }
 }

@@ -111,19 +111,29 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
     const float h[4] = {lo_bf(hh.x), hi_bf(hh.x), lo_bf(hh.y), hi_bf(hh.y)};
     if (p.dact == 1) {
       for (int r = 0; r < 4; ++r) v[r] *= dgelu_tanh(h[r]);
-    } else {
+    } else if (p.dact == 2) {
       for (int r = 0; r < 4; ++r) v[r] *= dgelu_erf(h[r]);
+    } else {  // 3: pre_in already holds gelu'(x)
+      for (int r = 0; r < 4; ++r) v[r] *= h[r];
     }
   }
   if (p.act) {
+    float d[4];
+    if (p.act == 1 || p.act == 2) {
+      for (int r = 0; r < 4; ++r) d[r] = v[r];
+      if (p.act == 1) {
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      } else {
+        for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+      }
+    } else if (p.act == 3) {
+      for (int r = 0; r < 4; ++r) gelu_dgelu_tanh(v[r], v[r], d[r]);
+    } else {
+      for (int r = 0; r < 4; ++r) gelu_dgelu_erf(v[r], v[r], d[r]);
+    }
     if (p.pre_out) {
       *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n) =
-          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-    }
-    if (p.act == 1) {
-      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-    } else {
-      for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+          make_uint2(pack2(d[0], d[1]), pack2(d[2], d[3]));
     }
   }
   if (p.has_drop) {
@@ -152,14 +162,19 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
 enum {
   EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5,
   EPI_RES = 6,  // C = AB + residual (in-place gradient accumulation: residual == C)
-  EPI_BIAS_ACT_ERF = 7, EPI_DACT_ERF = 8  // 3 / 4 are the tanh-GELU forms
+  EPI_BIAS_ACT_ERF = 7, EPI_DACT_ERF = 8,  // 3 / 4 are the tanh-GELU forms
+  // GELU forward storing gelu'(x) (act 3 / 4) and the backward multiply by it (dact 3)
+  EPI_BIAS_ACT_D = 9, EPI_BIAS_ACT_ERF_D = 10, EPI_MUL = 11
 };
+constexpr int EPI_KINDS = 12;
 
 template <int EPI>
 struct EpiKind {
-  static constexpr bool ACT = EPI == EPI_BIAS_ACT || EPI == EPI_BIAS_ACT_ERF;
-  static constexpr bool DACT = EPI == EPI_DACT || EPI == EPI_DACT_ERF;
-  static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF;
+  static constexpr bool DERIV = EPI == EPI_BIAS_ACT_D || EPI == EPI_BIAS_ACT_ERF_D;
+  static constexpr bool ACT = EPI == EPI_BIAS_ACT || EPI == EPI_BIAS_ACT_ERF || DERIV;
+  static constexpr bool MUL = EPI == EPI_MUL;
+  static constexpr bool DACT = EPI == EPI_DACT || EPI == EPI_DACT_ERF || MUL;
+  static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF || EPI == EPI_BIAS_ACT_ERF_D;
   static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT;
   static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES;
   static constexpr bool AUX = DACT || RES;  // reads a bf16 [M, N] operand (pre_in / residual)
@@ -223,13 +238,19 @@ static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t 
     if constexpr (KD::DACT) {
       const float h[4] = {lo_bf(ax.x), hi_bf(ax.x), lo_bf(ax.y), hi_bf(ax.y)};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] *= KD::ERF ? dgelu_erf(h[r]) : dgelu_tanh(h[r]);
+      for (int r = 0; r < 4; ++r)
+        v[r] *= KD::MUL ? h[r] : KD::ERF ? dgelu_erf(h[r]) : dgelu_tanh(h[r]);
     }
-    if constexpr (KD::ACT) {  // the caller stores the pre-activation (16-B stores)
+    if constexpr (KD::ACT) {  // the caller stores pre (x, or gelu'(x)) with 16-B stores
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pre[r] = v[r];
-        v[r] = KD::ERF ? gelu_erf(v[r]) : gelu_tanh(v[r]);
+        if constexpr (KD::DERIV) {
+          if constexpr (KD::ERF) gelu_dgelu_erf(v[r], v[r], pre[r]);
+          else gelu_dgelu_tanh(v[r], v[r], pre[r]);
+        } else {
+          pre[r] = v[r];
+          v[r] = KD::ERF ? gelu_erf(v[r]) : gelu_tanh(v[r]);
+        }
       }
     }
     if constexpr (KD::RES) {

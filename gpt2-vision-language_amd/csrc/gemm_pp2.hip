@@ -354,6 +354,9 @@ int launch_pp3_epi(const GemmP& p, hipStream_t s) {
     case EPI_RES: return launch_pp3<NS, AMN, BMN, EPI_RES>(p, s);
     case EPI_BIAS_ACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF>(p, s);
     case EPI_DACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_DACT_ERF>(p, s);
+    case EPI_BIAS_ACT_D: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_D>(p, s);
+    case EPI_BIAS_ACT_ERF_D: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF_D>(p, s);
+    case EPI_MUL: return launch_pp3<NS, AMN, BMN, EPI_MUL>(p, s);
     default: return launch_pp2<4, 1, AMN, BMN>(p, s);
   }
 }
@@ -395,8 +398,14 @@ int gemm_epi_kind(const GemmP& p) {
     if (b && r) return EPI_BIAS_RES;
     return EPI_RES;
   }
-  if (p.act && !p.dact && b && !r) return p.act == 1 ? EPI_BIAS_ACT : EPI_BIAS_ACT_ERF;
-  if (p.dact && !p.act && !b && !r) return p.dact == 1 ? EPI_DACT : EPI_DACT_ERF;
+  if (p.act && !p.dact && b && !r) {
+    const int k[5] = {EPI_GEN, EPI_BIAS_ACT, EPI_BIAS_ACT_ERF, EPI_BIAS_ACT_D, EPI_BIAS_ACT_ERF_D};
+    return k[p.act];
+  }
+  if (p.dact && !p.act && !b && !r) {
+    const int k[4] = {EPI_GEN, EPI_DACT, EPI_DACT_ERF, EPI_MUL};
+    return k[p.dact];
+  }
   return EPI_GEN;
 }
 

@@ -81,6 +81,10 @@ def pad_vocab(w):
 # data-parallel bucketing (gvl.dist) in its place.  Tied parameters (wte: embedding +
 # lm_head) keep the autograd path, which sums both uses before one AccumulateGrad.
 FUSE_GRAD_ACC = True
+# MLP GELU: the forward epilogue stores gelu'(x) instead of x (GEMM act 3/4) and the backward
+# multiplies by it (dact 3), so the dX epilogue runs no transcendentals.  0 (GVL_GELU_DERIV=0)
+# stores x and recomputes gelu'(x) in the dX epilogue (act 1/2, dact 1/2).
+GELU_DERIV = 0 if os.environ.get("GVL_GELU_DERIV", "1") == "0" else 2
 _READY_HOOKS = []
 
 
@@ -194,8 +198,9 @@ class GPTBlockFn(torch.autograd.Function):
         y2 = y.view(B * T, C)
         xm = K.linear(y2, aproj_w, aproj_b, residual=x2)
         xn2, m2, r2 = K.layernorm_fwd(xm, ln2_w, ln2_b)
+        # the c_fc epilogue stores gelu'(x) (act 3) for the backward's dGELU multiply
         hpre = torch.empty(B * T, fc_w.shape[0], dtype=BF16, device=x.device)
-        h = K.linear(xn2, fc_w, fc_b, act=1, pre_out=hpre)
+        h = K.linear(xn2, fc_w, fc_b, act=1 + GELU_DERIV, pre_out=hpre)
         out = K.linear(h, mproj_w, mproj_b, residual=xm)
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(x2, xn1, m1, r1, qkv, y, lse, xm, xn2, m2, r2, hpre, h, ln1_w,
@@ -220,7 +225,7 @@ class GPTBlockFn(torch.autograd.Function):
         # MLP c_proj
         g[11] = _wgrad(ctx, 11, P[11], d2, h)
         g[12] = _bgrad(ctx, 12, P[12], d2)
-        dpre = K.linear_dx(d2, mproj_w, dact=1, pre_in=hpre)
+        dpre = K.linear_dx(d2, mproj_w, dact=3 if GELU_DERIV else 1, pre_in=hpre)
         g[9] = _wgrad(ctx, 9, P[9], dpre, xn2)
         g[10] = _bgrad(ctx, 10, P[10], dpre)
         dxn2 = K.linear_dx(dpre, fc_w)
@@ -338,7 +343,7 @@ class MLPFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(BF16).contiguous()
         hpre = torch.empty(x2.shape[0], w1.shape[0], dtype=BF16, device=x.device)
-        h = K.linear(x2, w1, b1, act=act, pre_out=hpre)
+        h = K.linear(x2, w1, b1, act=act + GELU_DERIV, pre_out=hpre)  # pre_out <- gelu'(x)
         r2 = residual.reshape(-1, w2.shape[0]).to(BF16).contiguous() if residual is not None else None
         y = K.linear(h, w2, b2, residual=r2, drop_p=drop_p, seed=seed, seed_ptr=_off(h, drop_p))
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
@@ -359,7 +364,7 @@ class MLPFn(torch.autograd.Function):
         P = ctx.params
         dw2 = _wgrad(ctx, 3, P[3], d2, h)
         db2 = _bgrad(ctx, 4, P[4], d2)
-        dpre = K.linear_dx(d2, w2, dact=act, pre_in=hpre)
+        dpre = K.linear_dx(d2, w2, dact=3 if GELU_DERIV else act, pre_in=hpre)
         dw1 = _wgrad(ctx, 1, P[1], dpre, x2)
         db1 = _bgrad(ctx, 2, P[2], dpre)
         dx = K.linear_dx(dpre, w1).view(shp) if _need(ctx, 0) else None

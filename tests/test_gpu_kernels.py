@@ -99,6 +99,32 @@ def test_gemm_persistent_epilogues(cuda, a_mn, b_mn, epi, M, N, K):
         assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(4104, 2312, 160), (16384, 768, 64), (300, 392, 96)])
+@pytest.mark.parametrize("act", [3, 4])
+def test_gemm_gelu_derivative_epilogues(cuda, M, N, K, act):
+    """act 3/4: GELU (tanh/erf) with pre_out <- gelu'(x) (what the MLP backward multiplies
+    by); dact 3: C = AB * pre_in.  Persistent (256- and 192-wide tiles) and ring kernels."""
+    K_ = _k()
+    torch.manual_seed(M + N + K + act)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.1).to(BF)
+    bias = torch.randn(N).to(BF)
+    A, B = a.to(cuda), b.t().contiguous().to(cuda)
+    x = (a.float() @ b.float() + bias.float()).requires_grad_(True)
+    g = O.gelu_tanh(x) if act == 3 else O.gelu_erf(x)
+    g.sum().backward()
+    d = torch.empty(M, N, dtype=BF, device=cuda)
+    y = K_.gemm(A, B, bias=bias.to(cuda), act=act, pre_out=d)
+    assert rel_err(y.float().cpu().numpy(), g.detach().numpy()) < 8e-3
+    assert rel_err(d.float().cpu().numpy(), x.grad.numpy()) < 8e-3
+    # backward multiply: dY @ W2 (MN-major B) * stored derivative
+    dy = torch.randn(M, K).to(BF)
+    w2 = (torch.randn(N, K) * 0.1).to(BF)  # nn.Linear(N -> K) weight [K, N] viewed as [N, K]^T
+    z = K_.gemm(dy.to(cuda), w2.t().contiguous().to(cuda), b_mn=True, dact=3, pre_in=d)
+    ref = (dy.float() @ w2.float().t()) * d.float().cpu()
+    assert rel_err(z.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
 def _kernel_name(A, B, a_mn, b_mn, M, N, K):
     import ctypes as C
     from gvl import _lib
