@@ -63,10 +63,14 @@ GVL_DEV void tile_of_block(const AttnP& p, int64_t ntile, int64_t& t, int64_t& h
   h = rem - b * p.H;
 }
 
-// [64 rows][64 d] bf16 tile, 128-B rows.  Row image for ds_read_b128 fragments.
-GVL_DEV int swz_row(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
-// Image for ds_read_b64_tr_b16-only tiles (V in the forward): conflict-free transposed reads.
+// [64 rows][64 d] bf16 tile, 128-B rows, 16-B chunk c of row r at c ^ (((r >> 1) & 3) << 1).
+// This one XOR is conflict-free for both fragment reads the kernels issue on a tile: the
+// ds_read_b128 row fragments (frag_row) and the ds_read_b64_tr_b16 transposed ones (frag_tr),
+// checked lane group by lane group (tools/attn_swizzle_check.py).  Round 1 used
+// c ^ ((r >> 1) & 7) for row-read tiles, which is 2-way conflicted on the transposed reads the
+// backward issues on Q, dO and K (PMC: 20-25 % of the dK/dV and dQ kernels' LDS cycles).
 GVL_DEV int swz_tr(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
+GVL_DEV int swz_row(int row, int chunk) { return swz_tr(row, chunk); }
 
 // Register-stage a 64x64 tile (rows r0.., valid rows < R) from a strided tensor.
 GVL_DEV void load_rows(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t r0, int64_t R, int tid) {
