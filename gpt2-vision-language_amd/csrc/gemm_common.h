@@ -31,6 +31,10 @@ struct GemmP {
   int64_t kper;
   float* ws;
   int64_t ws_bytes;
+  // in-launch two-way split-K combine (gemm_pp3_kernel): per-(tile, wave) arrival tickets,
+  // zero between calls; null -> partials go to gemm_splitk_reduce
+  uint32_t* tickets;
+  int64_t nticket;
 };
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
@@ -371,6 +375,72 @@ GVL_DEV void gemm_store_partial(const GemmP& p, const float4_t (&acc)[FM][FN], i
         *reinterpret_cast<float4*>(base + m * p.N + n) =
             make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     }
+  }
+}
+
+// In-launch combine of a tile's two K-halves (splits == 2), per wave, lock-free: each wave
+// publishes its 128 x BN/4 fp32 partial with write-through (sc1) 16-B stores, drains them
+// (vmcnt(0)), then lane 0 takes an agent-scope ticket for (tile, wave).  The wave drawing
+// ticket 1 arrived last: it reads the other half's partial with sc1 loads, adds it and runs
+// the epilogue; it also returns the ticket to 0 for the next call.  Nobody waits, so no
+// residency assumption; two-term fp32 addition is commutative, so the result does not
+// depend on which half arrives last (cdna_hip_programming.md §6 Guideline 16, counter form).
+typedef __attribute__((address_space(1))) uint32_t gvl_gu32_t;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// Addressing: the lane part of the offset is one VGPR ((lane & 15) rows, 4 (lane >> 4) cols);
+// the fragment / tile part is uniform and goes to soffset (tile-dependent, so the compiler
+// does not hoist 32 offsets out of the persistent loop and spill them).
+template <int FM, int FN>
+GVL_DEV bool gemm_splitk_arrive(const GemmP& p, const float4_t (&acc)[FM][FN], int split,
+                                int tile, int wave, int64_t mw0, int64_t nw0, int lane,
+                                __amdgpu_buffer_rsrc_t rw) {
+  const int voff = (int)(((int64_t)(lane & 15) * p.N + 4 * (lane >> 4)) * 4);
+  const int64_t base = (int64_t)split * p.M * p.N + mw0 * p.N + nw0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const bool mok = mw0 + i * 16 + (lane & 15) < p.M;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int soff = __builtin_amdgcn_readfirstlane((int)((base + (int64_t)i * 16 * p.N + j * 16) * 4));
+      if (mok && nw0 + j * 16 < p.N)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), rw, voff,
+                                               soff, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  gvl_gu32_t* t = (gvl_gu32_t*)(p.tickets + (int64_t)tile * 8 + wave);
+  uint32_t got = 0;
+  if (lane == 0) got = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  got = __builtin_amdgcn_readfirstlane(got);
+  if (got == 0) return false;
+  if (lane == 0) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Last arriver: acc += the other half's partial (sc1 loads, 2 x FN 16-B loads in flight;
+// rows past M are read unguarded inside the workspace and never stored).
+template <int FM, int FN>
+GVL_DEV void gemm_splitk_gather(const GemmP& p, float4_t (&acc)[FM][FN], int split,
+                                int64_t mw0, int64_t nw0, int lane, __amdgpu_buffer_rsrc_t rw) {
+  const int voff = (int)(((int64_t)(lane & 15) * p.N + 4 * (lane >> 4)) * 4);
+  const int64_t base = (int64_t)(1 - split) * p.M * p.N + mw0 * p.N + nw0;
+  constexpr int H = 2;  // fragment rows per batch of loads (register budget: acc is live)
+#pragma unroll
+  for (int h = 0; h < FM / H; ++h) {
+    u32x4_t t[H][FN];
+#pragma unroll
+    for (int i = 0; i < H; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int soff = __builtin_amdgcn_readfirstlane(
+            (int)((base + (int64_t)(h * H + i) * 16 * p.N + j * 16) * 4));
+        t[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rw, voff, soff, 16);
+      }
+#pragma unroll
+    for (int i = 0; i < H; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[h * H + i][j] += __builtin_bit_cast(float4_t, t[i][j]);
   }
 }
 

@@ -269,10 +269,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   pre.load_bias(p, cu_n0 + bcol, lane);
 #define GVL_PP3_EPILOGUE()                                                                   \
   do {                                                                                       \
-    if (p.splits > 1)                                                                        \
+    bool epi_ = true;                                                                        \
+    if (p.splits == 2 && p.tickets != nullptr) { /* two-way split-K combined in-launch */    \
+      const int tile_ = (int)(cu_m0 / BM) * p.tiles_n + (int)(cu_n0 / BN);                   \
+      const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws, p.ws_bytes);                      \
+      epi_ = gemm_splitk_arrive<FM, FN>(p, acc, cu_sp, tile_, wave, cu_m0 + arow,            \
+                                        cu_n0 + bcol, lane, rw);                             \
+      if (epi_) gemm_splitk_gather<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane, rw); \
+    } else if (p.splits > 1) {                                                               \
       gemm_store_partial<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane);           \
-    else                                                                                     \
-      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre);    \
+      epi_ = false;                                                                          \
+    }                                                                                        \
+    if (epi_) gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre); \
   } while (0)
 
   short8_t af[FM], bf[FN];
@@ -332,7 +340,7 @@ int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
   const int total = p.tiles_m * p.tiles_n * p.splits;
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
   gvl::launch_timed(kern, dim3(grid), dim3(512), lds, s, p);
-  if (p.splits > 1) gvl::gemm_splitk_reduce_launch(p, s);
+  if (p.splits > 1 && !(p.splits == 2 && p.tickets)) gvl::gemm_splitk_reduce_launch(p, s);
   return 0;
 }
 
@@ -344,7 +352,8 @@ int launch_pp3(const GemmP& p, hipStream_t s) {
 
 template <int NS, bool AMN, bool BMN>
 int launch_pp3_epi(const GemmP& p, hipStream_t s) {
-  if (p.splits > 1) return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);  // partials only
+  // partials only (the reduce kernel applies the epilogue) unless combined in-launch
+  if (p.splits > 1 && !(p.splits == 2 && p.tickets)) return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);
   switch (gvl::gemm_epi_kind(p)) {
     case EPI_PLAIN: return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);
     case EPI_BIAS: return launch_pp3<NS, AMN, BMN, EPI_BIAS>(p, s);
@@ -460,16 +469,52 @@ static int pp3_tile_width(int64_t M, int64_t N) {
   return e192 > e256 ? 192 : 256;
 }
 
+// Tile width and K split for shapes whose slab split-K choice is at most two-way, when the
+// two halves can meet inside the launch: estimated time in units of one 256x256 32-deep
+// K-step, rounds(items) * (steps per item + 6) * tile cost + ~4 for the combine (the last
+// arriver's write-through partial store and the other half's read).  A 192-wide step counts
+// 0.75 / 0.9 of a 256-wide one (pp3_tile_width).  M = 8064, N = 768 (caption decoder):
+// 128 tiles of 256x192 split in two = 256 items, one per CU.
+static void pp3_choose_combined(GemmP& p, int gran) {
+  const int64_t cus = num_cus(), tm = (p.M + 255) / 256;
+  double best = 1e30;
+  for (int bn : {256, 192}) {
+    if (bn == 192 && (p.N % 64 != 0 || p.N < 384 || gran != KS)) continue;
+    const double w = bn == 256 ? 1.0 : 0.75 / 0.9;
+    const int64_t tiles = tm * ((p.N + bn - 1) / bn);
+    for (int s = 1; s <= 2; ++s) {
+      if (s == 2 && (p.K % (2 * gran) != 0 || p.K / 2 < 256 || tiles * 8 > p.nticket ||
+                     2 * p.M * p.N * 4 > p.ws_bytes))
+        continue;
+      const int64_t rounds = (tiles * s + cus - 1) / cus;
+      const double t = (double)rounds * ((double)p.K / (32.0 * s) + 6.0) * w + (s == 2 ? 4.0 : 0.0);
+      if (t < best * 0.97) {
+        best = t;
+        p.bn = bn;
+        p.splits = s;
+      }
+    }
+  }
+  p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
+  p.kper = p.K / p.splits;
+}
+
 bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
   p.tiles_m = (int)((p.M + 255) / 256);
   p.tiles_n = (int)((p.N + 255) / 256);
   p.splits = 1;
-  if (p.ws != nullptr) {
-    const int sp = gemm_pp3_splits(p.M, p.N, p.K, gran);
-    if (sp > 1 && (int64_t)sp * p.M * p.N * 4 <= p.ws_bytes) p.splits = sp;
+  int sp = 1;
+  if (p.ws != nullptr) sp = gemm_pp3_splits(p.M, p.N, p.K, gran);
+  if (sp <= 2 && p.ws != nullptr && p.tickets != nullptr && gemm_epi_kind(p) != EPI_GEN) {
+    p.bn = 256;
+    pp3_choose_combined(p, gran);
+    if (force) return true;
+    return (int64_t)p.tiles_m * p.tiles_n * p.splits >= pp3_min_items();
   }
+  p.tickets = nullptr;  // slab split-K (gemm_splitk_reduce) or no split
+  if (sp > 1 && (int64_t)sp * p.M * p.N * 4 <= p.ws_bytes) p.splits = sp;
   p.kper = p.K / p.splits;
   if (p.splits == 1 && gemm_epi_kind(p) == EPI_GEN) return false;
   p.bn = 256;

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 4  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 5  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -37,6 +37,7 @@ class GemmDesc(C.Structure):
         ("c_fp32", c_i32),
         ("workspace", c_vp), ("workspace_bytes", c_i64),
         ("seed_ptr", c_vp),
+        ("tickets", c_vp), ("ticket_count", c_i64),
     ]
 
 

@@ -46,6 +46,7 @@ class GraphedStep:
         dev = next(model.parameters()).device
         self.seed_off = K.seed_offset(dev)
         K._gemm_workspace(dev)
+        K._gemm_tickets(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):

@@ -9,6 +9,8 @@ from __future__ import annotations
 import ctypes as C
 import math
 
+import os
+
 import torch
 
 from . import _lib
@@ -95,6 +97,24 @@ def _gemm_workspace(device):
     return ws
 
 
+_TK = {}
+GEMM_TICKETS = 1 << 16
+# In-launch two-way split-K combine (gvl.h ABI v5 tickets): measured slower than whole-K
+# tiles on the caption step's N = 768 GEMMs, so off unless GVL_PP3_COMBINE=1.
+SPLIT_COMBINE = os.environ.get("GVL_PP3_COMBINE", "0") == "1"
+
+
+def _gemm_tickets(device):
+    """Per-device arrival tickets of the in-launch two-way split-K combine (gvl.h ABI v5):
+    zero-filled once; every GEMM call leaves them zero again."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = _TK.get(key)
+    if t is None:
+        t = torch.zeros(GEMM_TICKETS, dtype=torch.int32, device=device)
+        _TK[key] = t
+    return t
+
+
 # ------------------------------------------------------------- device dropout offset
 _SEED_OFF = {}
 
@@ -151,6 +171,9 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     d.c_fp32 = int(out.dtype == F32)
     ws = _gemm_workspace(a.device)
     d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    if SPLIT_COMBINE:
+        tk = _gemm_tickets(a.device)
+        d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
     if _timer is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

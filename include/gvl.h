@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 4
+#define GVL_ABI_VERSION 5
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -82,6 +82,12 @@ typedef struct gvl_gemm_desc {
   void* workspace;        /* optional fp32 scratch for split-K (few output tiles, long K) */
   int64_t workspace_bytes;
   const uint64_t* seed_ptr; /* optional device step offset re-keying `seed` (see below) */
+  /* ABI v5: optional arrival tickets for the in-launch two-way split-K combine (the two
+   * K-halves of an output tile meet inside one launch; no separate reduce kernel).  The
+   * caller allocates them zero-filled once; every call leaves them zero again.  Needs
+   * ticket_count >= 8 * output tiles of the split GEMM; fewer -> the two-kernel path. */
+  uint32_t* tickets;
+  int64_t ticket_count;
 } gvl_gemm_desc;
 int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):

@@ -125,7 +125,7 @@ def test_gemm_gelu_derivative_epilogues(cuda, M, N, K, act):
     assert rel_err(z.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
-def _kernel_name(A, B, a_mn, b_mn, M, N, K):
+def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False):
     import ctypes as C
     from gvl import _lib
     d = _lib.GemmDesc()
@@ -133,6 +133,11 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K):
     d.m, d.n, d.k = M, N, K
     d.lda, d.ldb, d.ldc = A.stride(0), B.stride(0), N
     d.a_mn, d.b_mn = a_mn, b_mn
+    if tickets:  # as gvl.kernels.gemm passes them (workspace + in-launch combine tickets)
+        K_ = _k()
+        ws, tk = K_._gemm_workspace(A.device), K_._gemm_tickets(A.device)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+        d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
     buf = C.create_string_buffer(128)
     _lib.lib().gvl_gemm_kernel_name(C.byref(d), buf, 128)
     return buf.value.decode()
@@ -221,6 +226,63 @@ def test_gemm_tile192(cuda, a_mn, b_mn, epi, M, N, K):
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "res_inplace", "bias_act_d", "mul", "dact_erf"])
+@pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 768), (7992, 768, 2304)])
+def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
+    """The caption decoder's N = 768 GEMMs at M = 8064: 128 tiles of 256x192, each K split in
+    two halves that meet inside the launch (write-through partials + per-(tile, wave) arrival
+    tickets; the last arriver adds and runs the epilogue).  Every layout and epilogue kind,
+    ragged M; the result is bitwise reproducible (two-term fp32 sums commute, whichever half
+    arrives last) and the tickets are all zero again afterwards."""
+    K_ = _k()
+    torch.manual_seed(M + N + K + len(epi) + 5 * a_mn + 11 * b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
+    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192>"), name
+    h = a.float() @ b.float()
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    kw, ref = {}, h
+    if epi == "bias_res":
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "res_inplace":
+        kw, ref = dict(residual=None, out=None), h + res.float()
+    elif epi == "bias_act_d":
+        x = (h + bias.float()).requires_grad_(True)
+        g = O.gelu_erf(x)
+        g.sum().backward()
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=4, pre_out=pre), g.detach()
+    elif epi == "mul":
+        d = torch.randn(M, N).to(BF)
+        kw, ref = dict(dact=3, pre_in=d.to(cuda)), h * d.float()
+    elif epi == "dact_erf":
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_erf(hx).sum().backward()
+        kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
+    outs = []
+    K_.SPLIT_COMBINE = True
+    try:
+        for _ in range(2):
+            if epi == "res_inplace":
+                acc = res.to(cuda)
+                kw = dict(residual=acc, out=acc)
+            outs.append(K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw))
+    finally:
+        K_.SPLIT_COMBINE = False
+    torch.cuda.synchronize()
+    assert rel_err(outs[0].float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    assert torch.equal(outs[0], outs[1])
+    if epi == "bias_act_d":
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
+    assert int(K_._gemm_tickets(A.device).abs().sum()) == 0
 
 
 @pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
