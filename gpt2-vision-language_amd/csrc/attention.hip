@@ -593,6 +593,158 @@ __global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG
   }
 }
 
+// Short sequences (Tq, Tk <= 64: the caption decoder's 63 tokens, the Q-Former's 32 queries
+// over 32 / 33 tokens): the whole backward of one (b, h) in one block, no recompute.
+// Q, K, V, dO land in LDS once; phase 1 (wave w = queries 16w..16w+15) computes D = rowsum(dO O),
+// S, P, dP, dS exactly as the dQ kernel, writes dQ, and leaves P (dropped) and dS in LDS as
+// [query][key] tiles; phase 2 (wave w = keys 16w..16w+15) reads them transposed
+// (ds_read_b64_tr_b16 gives the same permuted k-slot order as the dK/dV kernel's registers) for
+// dV = P^T dO and dK = dS^T Q.  One launch instead of three, and S / dP computed once.
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
+  // [Q, K, V, dO, P, dS] 64x64 bf16 tiles
+  __shared__ __attribute__((aligned(16))) char smem[6][KT * D * 2];
+  char* const qs = smem[0];
+  char* const ks = smem[1];
+  char* const vs = smem[2];
+  char* const ds = smem[3];
+  char* const ps = smem[4];
+  char* const ss = smem[5];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Gl = lane >> 4;
+  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
+  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
+  {
+    uint4 r[2];
+    load_rows(r, qbase, p.q_st, 0, p.Tq, tid);
+    store_rows<false>(r, qs, tid);
+    load_rows(r, kbase, p.k_st, 0, p.Tk, tid);
+    store_rows<false>(r, ks, tid);
+    load_rows(r, vbase, p.v_st, 0, p.Tk, tid);
+    store_rows<false>(r, vs, tid);
+    load_rows(r, dobase, gg.do_st, 0, p.Tq, tid);
+    store_rows<false>(r, ds, tid);
+  }
+  // phase 1: this lane's query, its D (4 lanes x 16 dims of dO . O) and log-sum-exp
+  const int ql = wave * 16 + (lane & 15);
+  const bool qok = ql < p.Tq;
+  const int64_t ridx = bh * p.Tq + ql;
+  float Dq = 0.f, lse2 = 0.f;
+  short8_t qf[2], df[2];
+  if (qok) {
+    const uint4* orow = reinterpret_cast<const uint4*>(obase + ql * p.o_st + 16 * Gl);
+    const uint4* drow = reinterpret_cast<const uint4*>(dobase + ql * gg.do_st + 16 * Gl);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint4 a = orow[c], d = drow[c];
+      Dq += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
+            hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
+            lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
+    }
+    lse2 = p.lse[ridx] * LOG2E;
+  }
+  Dq += __shfl_xor(Dq, 16, 64);
+  Dq += __shfl_xor(Dq, 32, 64);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    qf[s2] = load_frag_global(qbase + ql * p.q_st, s2, lane, qok);
+    df[s2] = load_frag_global(dobase + ql * gg.do_st, s2, lane, qok);
+  }
+  __syncthreads();
+  float4_t sc[4], dp[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+    dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      sc[n] = mfma16(frag_row(ks, 16 * n, s2, lane), qf[s2], sc[n]);
+      dp[n] = mfma16(frag_row(vs, 16 * n, s2, lane), df[s2], dp[n]);
+    }
+  }
+  const uint64_t drow0 = (uint64_t)ridx * (uint64_t)p.Tk;
+  float4_t pd[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kk = 16 * n + 4 * Gl + r;
+      float pv = __builtin_amdgcn_exp2f(fmaf(sc[n][r], p.c2, -lse2));
+      if (!qok || kk >= p.Tk || (p.causal && kk > ql)) pv = 0.f;
+      float pdrop = pv, dpv = dp[n][r];
+      if constexpr (DROP) {
+        const bool keep = rng_keep(seed_, drow0 + (uint64_t)kk, p.drop_thresh);
+        pdrop = keep ? pv * p.drop_scale : 0.f;
+        dpv = keep ? dpv * p.drop_scale : 0.f;
+      }
+      pd[n][r] = pdrop;
+      sc[n][r] = pv * (dpv - Dq);  // dS
+    }
+  // P and dS to LDS as [query][key]: lane (query ql) owns keys 16n + 4Gl .. +3 (8 bytes)
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int off = swz_tr(ql, 2 * n + (Gl >> 1)) + (Gl & 1) * 8;
+    *reinterpret_cast<uint2*>(ps + off) =
+        make_uint2(pack2(pd[n][0], pd[n][1]), pack2(pd[n][2], pd[n][3]));
+    *reinterpret_cast<uint2*>(ss + off) =
+        make_uint2(pack2(sc[n][0], sc[n][1]), pack2(sc[n][2], sc[n][3]));
+  }
+  {  // dQ = dS K (lane-local dS fragments, K read transposed)
+    const short8_t sf0 = pack_frag(sc[0], sc[1]), sf1 = pack_frag(sc[2], sc[3]);
+    float4_t acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = mfma16(frag_tr<false>(ks, t, 0, lane), sf0, float4_t{0.f, 0.f, 0.f, 0.f});
+      acc[t] = mfma16(frag_tr<false>(ks, t, 1, lane), sf1, acc[t]);
+    }
+    if (qok) {
+      bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + ql * gg.dq_st;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<uint2*>(dst + 16 * t + 4 * Gl) =
+            make_uint2(pack2(acc[t][0] * p.scale, acc[t][1] * p.scale),
+                       pack2(acc[t][2] * p.scale, acc[t][3] * p.scale));
+    }
+  }
+  __syncthreads();
+  // phase 2: this lane's key; P^T / dS^T fragments in the dK/dV kernel's k-slot order
+  const int kl = wave * 16 + (lane & 15);
+  float4_t dk[4], dv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const short8_t pf = frag_tr<false>(ps, wave, s2, lane);
+    const short8_t sf = frag_tr<false>(ss, wave, s2, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dv[t] = mfma16(frag_tr<false>(ds, t, s2, lane), pf, dv[t]);
+      dk[t] = mfma16(frag_tr<false>(qs, t, s2, lane), sf, dk[t]);
+    }
+  }
+  if (kl < p.Tk) {
+    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + kl * gg.dk_st;
+    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + kl * gg.dv_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(dkr + d) =
+          make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale),
+                     pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
+      *reinterpret_cast<uint2*>(dvr + d) =
+          make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+    }
+  }
+}
+
 int fill(const gvl_attn_desc* d, AttnP& p) {
   GVL_REQUIRE(d && d->q && d->k && d->v && d->o, "gvl_attn: null tensor");
   GVL_REQUIRE(d->B > 0 && d->H > 0 && d->Tq > 0 && d->Tk > 0, "gvl_attn: empty shape");
@@ -638,6 +790,16 @@ int dkdv_groups(int64_t Tk) {
     return (e && atoi(e) == 2) ? 2 : 1;
   }();
   return (g == 2 && Tk > 64) ? 2 : 1;
+}
+
+// Single-launch backward for Tq, Tk <= 64 (attn_bwd_short_kernel); GVL_ATTN_SHORT=0 restores the
+// three-kernel path (A/B measurement).
+bool short_bwd_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_ATTN_SHORT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // Block count of the 1-D heavy-first grid (see tile_of_block); fill() bounds it.
@@ -686,6 +848,13 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   g.dv_sb = gd->dv_sb; g.dv_st = gd->dv_st; g.dv_sh = gd->dv_sh;
   g.Dws = static_cast<float*>(gd->workspace);
   hipStream_t s = gvl::as_stream(stream);
+  if (d->Tq <= 64 && d->Tk <= 64 && short_bwd_enabled()) {
+    dim3 grid((unsigned)(d->B * d->H));
+    if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true>, grid, dim3(NT), 0, s, p, g);
+    else gvl::launch_timed(attn_bwd_short_kernel<false>, grid, dim3(NT), 0, s, p, g);
+    GVL_LAUNCH_CHECK("gvl_attn_bwd(short)");
+    return 0;
+  }
   const int64_t rows = d->B * d->H * d->Tq;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");

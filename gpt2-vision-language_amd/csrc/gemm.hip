@@ -195,6 +195,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
   p.splits = 1;
   p.bn = 256;
+  p.bm = 256;
   p.kper = d->k;
   p.group = env().group;
   p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
@@ -230,8 +231,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     } else if (gvl::gemm_pp3_plan(p, false)) {
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
-      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
-               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn);
+      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
+               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm);
     } else {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn)),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);

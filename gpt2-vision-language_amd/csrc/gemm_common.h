@@ -23,6 +23,7 @@ struct GemmP {
   uint32_t drop_thresh;
   int tiles_m, tiles_n;
   int bn;     // output tile width of the persistent kernel (256 or 192; gemm_pp3_plan)
+  int bm;     // output tile height of the persistent kernel (256, or 128 with bn 192)
   int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
@@ -459,6 +460,11 @@ int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
 int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels
 bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
+int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
+int gemm_pp3_launch_ff(const GemmP& p, hipStream_t s);  // gemm_pp3_{ff,ft,tf,tt}.hip
+int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);
+int gemm_pp3_launch_tf(const GemmP& p, hipStream_t s);
+int gemm_pp3_launch_tt(const GemmP& p, hipStream_t s);
 int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
 bool gemm_8p_plan(GemmP& p, bool force);
 bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);

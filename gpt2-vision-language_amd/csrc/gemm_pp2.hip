@@ -21,6 +21,7 @@
 #include "capi_util.h"
 #include "gemm_common.h"
 #include "gemm_ring.h"
+#include "gemm_pp3.h"
 #include "../../include/gvl.h"
 
 namespace {
@@ -148,228 +149,6 @@ int launch_pp2(const GemmP& p0, hipStream_t s) {
   return 0;
 }
 
-// Persistent variant (v5): grid = min(tiles, CUs); workgroup b walks tiles b, b+G, b+2G..
-// and the LDS ring runs straight across tile boundaries (the next tile's first K-steps are
-// already landing while the current tile finishes), so no tile pays a cold prologue.  A
-// tile's epilogue runs at the start of the next memory cluster M(c), i.e. while the partner
-// wave of the SIMD is in its compute cluster; its 16-B stores drain behind the following
-// MFMAs.  (vmcnt waits stay correct: stores and loads retire in issue order, so a counted
-// wait for K-step c+1 at most also waits for part of the stores issued after it.)
-// DMA addresses: per-lane offsets are computed once per tile; a K-step only adds a scalar
-// soffset.  The epilogue kind EPI is a template parameter so the loop carries only its ops.
-// Split-K: work item w = (tile w / splits, K-slice w % splits), every slice kper deep (the
-// host only splits when K divides evenly); slices store fp32 partials, gemm_splitk_reduce
-// applies the epilogue.  KC = 1, bf16 output.
-template <int BN, bool BMN>
-struct SlabB {
-  using type = Step<256, BMN, 8>;
-};
-template <bool BMN>
-struct SlabB<192, BMN> {
-  using type = Step192<BMN>;
-};
-
-// BN = 192 (FN = 3 fragments of 16 columns per wave): for N = 768 / 2304 outputs the 256-wide
-// tiles leave CUs idle in the last round (M = 16384, N = 768: 192 tiles on 256 CUs; 192-wide:
-// 256 tiles).  Its B slab is 12 DMA pieces: waves 0-3 (group 0) issue 2, waves 4-7 one, so
-// the counted waits use a per-group pieces-per-step count.
-template <int NS, bool AMN, bool BMN, int EPI, int BN = 256>
-__global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
-  constexpr int BM = 256, NW = 8, FM = 8, FN = BN / 64;
-  static_assert(NS >= 3 && NS <= 5, "ring geometry");
-  static_assert(BN == 256 || BN == 192, "tile width");
-  using SA = Step<BM, AMN, NW>;
-  using SB = typename SlabB<BN, BMN>::type;
-  constexpr int SLOT = SA::BYTES + SB::BYTES;
-  constexpr int IPW0 = SA::PER + SB::PER;                       // group 0 waves
-  constexpr int IPW1 = SA::PER + (BN == 256 ? SB::PER : 1);     // group 1 waves
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = wave >> 2, wc = wave & 3;
-
-  const int total = p.tiles_m * p.tiles_n * p.splits;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int ntl = (total - b + G - 1) / G;  // work items of this workgroup
-  const int nks = (int)(p.kper / KS);
-  const int nsteps = ntl * nks;
-  // work item of local item t: XCD-contiguous remap over the virtual grid of `total` items
-  // (G % 8 == 0 keeps b + tG on workgroup b's XCD), then the L2-grouped walk
-  auto tile_coords = [&](int t, int64_t& m0, int64_t& n0, int64_t& k0, int& split) {
-    const int vid = b + t * G;
-    const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
-    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
-    int tm, tn;
-    gemm_tile_of(work, p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
-    m0 = (int64_t)tm * BM;
-    n0 = (int64_t)tn * BN;
-    k0 = (int64_t)split * p.kper;
-  };
-
-  const int64_t a_rows = AMN ? p.K : p.M, b_rows = BMN ? p.K : p.N;
-  const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
-  const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
-  const int sa_step = SA::step_bytes(p.lda), sb_step = SB::step_bytes(p.ldb);
-  // issue cursor (steps are issued strictly in order)
-  int is_t = 0, is_k = 0;
-  int offa[SA::PER], offb[SB::PER];
-  {
-    int64_t m0, n0, k0;
-    int sp;
-    tile_coords(0, m0, n0, k0, sp);
-    SA::base_offsets(p.lda, m0, k0, wave, lane, offa);
-    SB::base_offsets(p.ldb, n0, k0, wave, lane, offb);
-  }
-
-#define GVL_PP3_ISSUE(gstep)                                                        \
-  do {                                                                              \
-    if ((gstep) < nsteps) {                                                         \
-      char* slot_ = smem + ((gstep) % NS) * SLOT;                                   \
-      SA::issue_at(ra, offa, is_k * sa_step, slot_, wave);                          \
-      SB::issue_at(rb, offb, is_k * sb_step, slot_ + SA::BYTES, wave);              \
-      if (++is_k == nks) {                                                          \
-        is_k = 0;                                                                   \
-        if (++is_t < ntl) {                                                         \
-          int64_t m0_, n0_, k0_;                                                    \
-          int sp_;                                                                  \
-          tile_coords(is_t, m0_, n0_, k0_, sp_);                                    \
-          SA::base_offsets(p.lda, m0_, k0_, wave, lane, offa);                      \
-          SB::base_offsets(p.ldb, n0_, k0_, wave, lane, offb);                      \
-        }                                                                           \
-      }                                                                             \
-    }                                                                               \
-  } while (0)
-
-  float4_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int arow = g * 128, bcol = wc * (BN / 4);
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i) GVL_PP3_ISSUE(i);
-  {
-    const int r = nsteps - 1, n = r < 0 ? 0 : (r < NS - 2 ? r : NS - 2);
-    if (g == 0) wait_vm_steps<IPW0, NS - 2>(n);
-    else wait_vm_steps<IPW1, NS - 2>(n);
-  }
-  barrier_lds();
-  if (g == 1) __builtin_amdgcn_s_barrier();
-
-  // alpha (x *alpha_ptr, a device scalar written before this launch) read once up front: a
-  // load inside the loop would make hipcc drain the DMA queue (vmcnt(0)) at every epilogue
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  int cu_t = 0, cu_k = 0;  // compute cursor
-  int64_t cu_m0, cu_n0, cu_k0;
-  int cu_sp;
-  tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp);
-  EpiPre<FM, FN, EPI> pre;
-  pre.load_bias(p, cu_n0 + bcol, lane);
-#define GVL_PP3_EPILOGUE()                                                                   \
-  do {                                                                                       \
-    bool epi_ = true;                                                                        \
-    if (p.splits == 2 && p.tickets != nullptr) { /* two-way split-K combined in-launch */    \
-      const int tile_ = (int)(cu_m0 / BM) * p.tiles_n + (int)(cu_n0 / BN);                   \
-      const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws, p.ws_bytes);                      \
-      epi_ = gemm_splitk_arrive<FM, FN>(p, acc, cu_sp, tile_, wave, cu_m0 + arow,            \
-                                        cu_n0 + bcol, lane, rw);                             \
-      if (epi_) gemm_splitk_gather<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane, rw); \
-    } else if (p.splits > 1) {                                                               \
-      gemm_store_partial<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane);           \
-      epi_ = false;                                                                          \
-    }                                                                                        \
-    if (epi_) gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre); \
-  } while (0)
-
-  short8_t af[FM], bf[FN];
-  for (int c = 0; c < nsteps; ++c) {
-    // ---- M(c): previous tile's epilogue, fragments of step c, DMA of step c+NS-1
-    if (cu_k == 0 && c > 0) {
-      GVL_PP3_EPILOGUE();
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-      ++cu_t;
-      tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp);
-      pre.load_bias(p, cu_n0 + bcol, lane);
-    }
-    const char* sl = smem + (c % NS) * SLOT;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = SB::frag(sl + SA::BYTES, bcol + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = SA::frag(sl, arow + 16 * i, lane);
-    GVL_PP3_ISSUE(c + NS - 1);
-    {
-      const int r = nsteps - (c + 2);  // steps issued but not needed by step c+1
-      if (g == 1) wait_vm_steps<IPW1, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
-    }
-    barrier_lds();
-    // ---- C(c)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    if (++cu_k == nks) cu_k = 0;
-    {
-      const int r = nsteps - (c + 2);
-      if (g == 0) wait_vm_steps<IPW0, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
-    }
-    barrier_lds();
-  }
-#undef GVL_PP3_ISSUE
-  if (g == 0) __builtin_amdgcn_s_barrier();
-  if (nsteps > 0) GVL_PP3_EPILOGUE();
-#undef GVL_PP3_EPILOGUE
-}
-
-template <int NS, bool AMN, bool BMN, int EPI, int BN>
-int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
-  GemmP p = p0;  // tiles_m/n, splits, kper set by gemm_pp3_try
-  constexpr int lds = NS * (256 + BN) * KS * 2;
-  auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI, BN>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
-  }
-  const int total = p.tiles_m * p.tiles_n * p.splits;
-  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
-  gvl::launch_timed(kern, dim3(grid), dim3(512), lds, s, p);
-  if (p.splits > 1 && !(p.splits == 2 && p.tickets)) gvl::gemm_splitk_reduce_launch(p, s);
-  return 0;
-}
-
-template <int NS, bool AMN, bool BMN, int EPI>
-int launch_pp3(const GemmP& p, hipStream_t s) {
-  return p.bn == 192 ? launch_pp3_bn<NS, AMN, BMN, EPI, 192>(p, s)
-                     : launch_pp3_bn<NS, AMN, BMN, EPI, 256>(p, s);
-}
-
-template <int NS, bool AMN, bool BMN>
-int launch_pp3_epi(const GemmP& p, hipStream_t s) {
-  // partials only (the reduce kernel applies the epilogue) unless combined in-launch
-  if (p.splits > 1 && !(p.splits == 2 && p.tickets)) return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);
-  switch (gvl::gemm_epi_kind(p)) {
-    case EPI_PLAIN: return launch_pp3<NS, AMN, BMN, EPI_PLAIN>(p, s);
-    case EPI_BIAS: return launch_pp3<NS, AMN, BMN, EPI_BIAS>(p, s);
-    case EPI_BIAS_RES: return launch_pp3<NS, AMN, BMN, EPI_BIAS_RES>(p, s);
-    case EPI_BIAS_ACT: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT>(p, s);
-    case EPI_DACT: return launch_pp3<NS, AMN, BMN, EPI_DACT>(p, s);
-    case EPI_RES: return launch_pp3<NS, AMN, BMN, EPI_RES>(p, s);
-    case EPI_BIAS_ACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF>(p, s);
-    case EPI_DACT_ERF: return launch_pp3<NS, AMN, BMN, EPI_DACT_ERF>(p, s);
-    case EPI_BIAS_ACT_D: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_D>(p, s);
-    case EPI_BIAS_ACT_ERF_D: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF_D>(p, s);
-    case EPI_MUL: return launch_pp3<NS, AMN, BMN, EPI_MUL>(p, s);
-    default: return launch_pp2<4, 1, AMN, BMN>(p, s);
-  }
-}
-
 // cfg 0: NS=4, KC=1 (3 steps in flight, 32-MFMA clusters); 1: NS=4, KC=2 (64-MFMA clusters,
 // ring drained per cluster); 2: NS=5, KC=2 (one step in flight across the cluster barrier).
 template <bool AMN, bool BMN>
@@ -377,7 +156,7 @@ int launch_layout(const GemmP& p, int cfg, hipStream_t s) {
   switch (cfg) {
     case 3: {
       GemmP q = p;
-      if (gvl::gemm_pp3_plan(q, true)) return launch_pp3_epi<4, AMN, BMN>(q, s);
+      if (gvl::gemm_pp3_plan(q, true) && gvl::gemm_pp3_launch(q, AMN, BMN, s) == 0) return 0;
       return launch_pp2<4, 1, AMN, BMN>(p, s);
     }
     case 1: return launch_pp2<4, 2, AMN, BMN>(p, s);
@@ -499,12 +278,38 @@ static void pp3_choose_combined(GemmP& p, int gran) {
   p.kper = p.K / p.splits;
 }
 
+// Tile height 128 (with 192-wide tiles) when its tiles fill the CUs in fewer rounds than the
+// 256-row tiles: estimated per-tile cost 0.375 / E128 of a 256x256 tile (E128 = per-FLOP
+// efficiency of the half-height tile, GVL_PP3_E128 x 100, default 70: measured equal to the
+// 128x128 ring at N = 768, 8 % slower than 256x192 at N = 2304); GVL_PP3_BM=128|256
+// forces the height (A/B).
+static int pp3_tile_height(int64_t M, int64_t N, int bn) {
+  static const int forced = [] {
+    const char* e = getenv("GVL_PP3_BM");
+    return e ? atoi(e) : 0;
+  }();
+  static const double e128 = [] {
+    const char* e = getenv("GVL_PP3_E128");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v / 100.0 : 0.70;
+  }();
+  if (N % 64 != 0 || N < 384) return 256;
+  if (forced == 256 || forced == 128) return forced;
+  const int64_t cus = num_cus();
+  auto rounds = [&](int64_t t) { return (double)((t + cus - 1) / cus); };
+  const double w_bn = bn == 256 ? 1.0 : 0.75 / 0.9;
+  const double t256 = rounds(((M + 255) / 256) * ((N + bn - 1) / bn)) * w_bn;
+  const double t128 = rounds(((M + 127) / 128) * ((N + 191) / 192)) * 0.375 / e128;
+  return t128 < 0.95 * t256 ? 128 : 256;
+}
+
 bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.c_f32 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
   p.tiles_m = (int)((p.M + 255) / 256);
   p.tiles_n = (int)((p.N + 255) / 256);
   p.splits = 1;
+  p.bm = 256;
   int sp = 1;
   if (p.ws != nullptr) sp = gemm_pp3_splits(p.M, p.N, p.K, gran);
   if (sp <= 2 && p.ws != nullptr && p.tickets != nullptr && gemm_epi_kind(p) != EPI_GEN) {
@@ -519,6 +324,11 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.splits == 1 && gemm_epi_kind(p) == EPI_GEN) return false;
   p.bn = 256;
   if (p.splits == 1 && gran == KS) p.bn = pp3_tile_width(p.M, p.N);
+  if (p.splits == 1 && gran == KS && pp3_tile_height(p.M, p.N, p.bn) == 128) {
+    p.bm = 128;
+    p.bn = 192;
+    p.tiles_m = (int)((p.M + 127) / 128);
+  }
   if (p.bn != 256) p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
   if (force) return true;
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
@@ -528,14 +338,17 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   return tiles * p.splits >= pp3_min_items();
 }
 
+int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s) {
+  if (!a_mn && !b_mn) return gemm_pp3_launch_ff(p, s);
+  if (!a_mn && b_mn) return gemm_pp3_launch_ft(p, s);
+  if (a_mn && !b_mn) return gemm_pp3_launch_tf(p, s);
+  return gemm_pp3_launch_tt(p, s);
+}
+
 bool gemm_pp3_try(const GemmP& p0, int a_mn, int b_mn, hipStream_t s) {
   GemmP p = p0;
   if (!gemm_pp3_plan(p, false)) return false;
-  if (!a_mn && !b_mn) launch_pp3_epi<4, false, false>(p, s);
-  else if (!a_mn && b_mn) launch_pp3_epi<4, false, true>(p, s);
-  else if (a_mn && !b_mn) launch_pp3_epi<4, true, false>(p, s);
-  else launch_pp3_epi<4, true, true>(p, s);
-  return true;
+  return gemm_pp3_launch(p, a_mn, b_mn, s) == 0;
 }
 
 int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s) {

@@ -1,0 +1,6 @@
+// gemm_pp3_kernel instances for A MN-contiguous, B K-contiguous (gemm_pp3.h).
+#include "gemm_pp3.h"
+
+namespace gvl {
+int gemm_pp3_launch_tf(const GemmP& p, hipStream_t s) { return launch_pp3_epi<4, true, false>(p, s); }
+}  // namespace gvl

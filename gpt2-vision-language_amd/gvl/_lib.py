@@ -124,7 +124,8 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        # GVL_LIB: an alternative build of the same library (A/B of compile-time variants)
+        p = path or os.environ.get("GVL_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise ImportError(
                 f"libgvl.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; "

@@ -204,7 +204,7 @@ def test_gemm_tile192(cuda, a_mn, b_mn, epi, M, N, K):
     b = (torch.randn(K, N) * 0.1).to(BF)
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
-    assert _kernel_name(A, B, a_mn, b_mn, M, N, K).endswith(", 192>")
+    assert ", 192, " in _kernel_name(A, B, a_mn, b_mn, M, N, K)  # 256- or 128-row tiles
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
@@ -244,7 +244,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
     name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
-    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192>"), name
+    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 256>"), name
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
@@ -283,6 +283,50 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
     assert int(K_._gemm_tickets(A.device).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "res_inplace", "bias_act_d", "mul", "dact"])
+@pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 768), (7992, 768, 32)])
+def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
+    """128x192 tiles of the persistent kernel (the caption decoder's N = 768 GEMMs at
+    M = 8064: 63 x 4 = 252 tiles, one round on 256 CUs): every layout (the 128-row A slab is
+    one DMA piece per wave) and epilogue kind, ragged M, a single K-step."""
+    K_ = _k()
+    torch.manual_seed(M + N + K + len(epi) + 3 * a_mn + 7 * b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    name = _kernel_name(A, B, a_mn, b_mn, M, N, K)
+    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
+    h = a.float() @ b.float()
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    kw, ref = {}, h
+    if epi == "bias_res":
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "res_inplace":
+        acc = res.to(cuda)
+        kw, ref = dict(residual=acc, out=acc), h + res.float()
+    elif epi == "bias_act_d":
+        x = (h + bias.float()).requires_grad_(True)
+        g = O.gelu_tanh(x)
+        g.sum().backward()
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=3, pre_out=pre), g.detach()
+    elif epi == "mul":
+        d = torch.randn(M, N).to(BF)
+        kw, ref = dict(dact=3, pre_in=d.to(cuda)), h * d.float()
+    elif epi == "dact":
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_tanh(hx).sum().backward()
+        kw, ref = dict(dact=1, pre_in=hpre.to(cuda)), h * hx.grad
+    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    if epi == "bias_act_d":
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
 
 
 @pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
