@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "capi_util.h"
+#include "gemm_ring.h"
 #include "../../include/gvl.h"
 
 namespace {
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
 // dK/dV: block = (64*G-key tile, head, batch), waves own G groups of 16 keys; loop over
 // 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
+__global__ __launch_bounds__(NT, G == 1 ? 3 : 1) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int KB = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
@@ -523,12 +524,6 @@ __global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG
       // lane holds S[q = q0 + 16n + 4Gl + r][key[g]]; lse and D of those 4 consecutive
       // queries come from LDS as one float4 each
       short8_t pf[G][2], sf[G][2];
-      float4 l4[4], d4[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        l4[n] = *reinterpret_cast<const float4*>(&sl[st][0][16 * n + 4 * Gl]);
-        d4[n] = *reinterpret_cast<const float4*>(&sl[st][1][16 * n + 4 * Gl]);
-      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int64_t kg_max = kblk0 + wave * 16 * G + g * 16 + 15;
@@ -536,12 +531,15 @@ __global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG
         const int qlim = (int)(p.Tq - q0), kq = (int)(key[g] - q0);
         float4_t pd[4];
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < 4; ++n) {
+          // lse / D of this lane's 4 queries, read where used (register budget: 3 waves/SIMD)
+          const float4 l4 = *reinterpret_cast<const float4*>(&sl[st][0][16 * n + 4 * Gl]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&sl[st][1][16 * n + 4 * Gl]);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qi = 16 * n + 4 * Gl + r;
-            const float lr = r == 0 ? l4[n].x : r == 1 ? l4[n].y : r == 2 ? l4[n].z : l4[n].w;
-            const float dr = r == 0 ? d4[n].x : r == 1 ? d4[n].y : r == 2 ? d4[n].z : d4[n].w;
+            const float lr = r == 0 ? l4.x : r == 1 ? l4.y : r == 2 ? l4.z : l4.w;
+            const float dr = r == 0 ? d4.x : r == 1 ? d4.y : r == 2 ? d4.z : d4.w;
             float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lr));
             if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
             float pdrop = pv, dpv = dp[g][n][r];
@@ -554,6 +552,7 @@ __global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG
             pd[n][r] = pdrop;
             sc[g][n][r] = pv * (dpv - dr);  // dS
           }
+        }
         pf[g][0] = pack_frag(pd[0], pd[1]);
         pf[g][1] = pack_frag(pd[2], pd[3]);
         sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
@@ -589,6 +588,353 @@ __global__ __launch_bounds__(NT, 3 - G) void attn_bwd_dkdv_kernel(AttnP p, AttnG
                      pack2(dk[g][t][2] * p.scale, dk[g][t][3] * p.scale));
       *reinterpret_cast<uint2*>(dvr + d) =
           make_uint2(pack2(dv[g][t][0], dv[g][t][1]), pack2(dv[g][t][2], dv[g][t][3]));
+    }
+  }
+}
+
+// dK/dV, LDS-DMA pipelined (default for Tk > 64): as attn_bwd_dkdv_kernel<1, DROP>, but the
+// Q / dO tiles and their lse / D rows move global -> LDS by buffer_load ... lds (no staging
+// registers) into a 3-slot ring, two query tiles ahead of the one being computed, with counted
+// vmcnt waits (PMC of the register-staged kernel: waves waiting 48 % of their cycles, LDS 5 %:
+// the one-tile-ahead register prefetch did not cover the load latency).  The DMA writes each
+// 64x64 tile lane-linearly in 1-KiB pieces (8 rows of 128 B); the swz_tr XOR is applied to
+// the source chunk, so the image is the same as store_rows'.  Rows past Tq read zero (buffer
+// bounds).  All LDS in one array (a second __shared__ object makes hipcc drain vmcnt before
+// the fragment reads).
+constexpr int DK_SLOT = 2 * KT * D * 2 + 2 * KT * 4;  // Q, dO tiles + lse2, D rows
+
+// frag_tr<false> by inline asm, without a wait: hipcc treats a ds_read_b64_tr_b16 builtin as
+// possibly aliasing any in-flight LDS DMA and drains vmcnt(0) in front of it.  The caller
+// waits (lds_wait8) before the MFMAs use the fragments.
+GVL_DEV short8_t frag_tr_asm(const char* lds, int t, int s, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = 2 * t + (p >> 1);
+  const int ra = 32 * s + 4 * G + q, rb = ra + 16;
+  const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
+  const uint32_t oa = base + swz_tr(ra, ch) + (p & 1) * 8, ob = base + swz_tr(rb, ch) + (p & 1) * 8;
+  short4_t lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
+               : "=v"(lo), "=v"(hi) : "v"(oa), "v"(ob) : "memory");
+  short8_t r;
+  r.lo = lo;
+  r.hi = hi;
+  return r;
+}
+// lgkmcnt(0), with the fragments threaded through so no use is scheduled above the wait
+GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
+                 "+v"(b[3])
+               :
+               : "memory");
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG gg) {
+  using gvl_ring::lds_void_t;
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
+  __shared__ __attribute__((aligned(16))) char smem[3 * DK_SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Gl = lane >> 4;
+  int64_t kt, h, b;
+  tile_of_block<false>(p, (p.Tk + KT - 1) / KT, kt, h, b);
+  const int64_t kblk0 = kt * KT;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  const int64_t rbase = (b * p.H + h) * p.Tq;
+  const int64_t key = kblk0 + wave * 16 + (lane & 15);
+  const bool kok = key < p.Tk;
+  short8_t kf[2], vf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    kf[s2] = load_frag_global(kbase + key * p.k_st, s2, lane, kok);
+    vf[s2] = load_frag_global(vbase + key * p.v_st, s2, lane, kok);
+  }
+  const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
+  const int nqt = (int)((p.Tq + KT - 1) / KT);
+  const int nq = nqt - qt_first;
+  float4_t dk[4], dv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // buffer resources (bounds = the last valid row's end: rows >= Tq read zero)
+  const __amdgpu_buffer_rsrc_t rq = gvl_ring::uniform_rsrc(qbase, ((p.Tq - 1) * p.q_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rd = gvl_ring::uniform_rsrc(dobase, ((p.Tq - 1) * gg.do_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rl = gvl_ring::uniform_rsrc(p.lse + rbase, p.Tq * 4);
+  const __amdgpu_buffer_rsrc_t rD = gvl_ring::uniform_rsrc(gg.Dws + rbase, p.Tq * 4);
+  // DMA instructions per wave per tile: 4 (+1 for waves 0 / 1: the lse / D row).  Wave w
+  // issues pieces 2w, 2w+1 (rows 8j .. 8j+7) of each tile; the lane offsets include the tile
+  // row q0 so they are recomputed per tile (not hoisted out of the loop and spilled).
+  auto issue = [&](int qt, int slot) {
+    char* sb = smem + slot * DK_SLOT;
+    const int64_t q0 = (int64_t)qt * KT;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = 2 * wave + t;
+      const int row = 8 * j + (lane >> 3);
+      const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+      const int voq = (int)(((q0 + row) * p.q_st + chunk * 8) * 2);
+      const int vod = (int)(((q0 + row) * gg.do_st + chunk * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_void_t*)(sb + j * 1024), 16, voq, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void_t*)(sb + KT * D * 2 + j * 1024), 16,
+                                               vod, 0, 0, 0);
+    }
+    if (wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void_t*)(sb + 2 * KT * D * 2), 4, lane * 4,
+                                               (int)(q0 * 4), 0, 0);
+    if (wave == 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void_t*)(sb + 2 * KT * D * 2 + KT * 4), 4,
+                                               lane * 4, (int)(q0 * 4), 0, 0);
+  };
+  // wait until all but the newest tile's DMA of this wave have landed (n = 1) or all (n = 0)
+  auto wait_tiles = [&](int n) {
+    if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (wave < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  };
+  if (nq > 0) {
+    issue(qt_first, 0);
+    if (nq > 1) issue(qt_first + 1, 1);
+    wait_tiles(nq > 1 ? 1 : 0);
+    gvl_ring::barrier_lds();
+  }
+  for (int i = 0; i < nq; ++i) {
+    const int qt = qt_first + i, st = i % 3;
+    if (i + 2 < nq) issue(qt + 2, (i + 2) % 3);
+    const char* qs = smem + st * DK_SLOT;
+    const char* ds = qs + KT * D * 2;
+    const float* sl = reinterpret_cast<const float*>(qs + 2 * KT * D * 2);
+    const int64_t q0 = (int64_t)qt * KT;
+    float4_t sc[4], dp[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+      dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        sc[n] = mfma16(frag_row(qs, 16 * n, s2, lane), kf[s2], sc[n]);
+        dp[n] = mfma16(frag_row(ds, 16 * n, s2, lane), vf[s2], dp[n]);
+      }
+    }
+    const int64_t kg_max = kblk0 + wave * 16 + 15;
+    const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
+    const int qlim = (int)(p.Tq - q0), kq = (int)(key - q0);
+    float4_t pd[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      // lse / D of this lane's 4 queries: read by inline asm, because hipcc cannot tell these
+      // bytes apart from the in-flight lse / D DMA of another slot and would drain vmcnt(0)
+      // (the whole two-ahead prefetch) before a plain read; they landed before the barrier.
+      float4_t l4, d4;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256\n\ts_waitcnt lgkmcnt(0)"
+                   : "=v"(l4), "=v"(d4)
+                   : "v"((uint32_t)reinterpret_cast<uintptr_t>(sl + 16 * n + 4 * Gl))
+                   : "memory");
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = 16 * n + 4 * Gl + r;
+        const float lr = l4[r] * LOG2E;
+        const float dr = d4[r];
+        float pv = __builtin_amdgcn_exp2f(fmaf(sc[n][r], p.c2, -lr));
+        if (msk && (!kok || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
+        float pdrop = pv, dpv = dp[n][r];
+        if constexpr (DROP) {
+          const bool keep = rng_keep(
+              seed_, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key, p.drop_thresh);
+          pdrop = keep ? pv * p.drop_scale : 0.f;
+          dpv = keep ? dpv * p.drop_scale : 0.f;
+        }
+        pd[n][r] = pdrop;
+        sc[n][r] = pv * (dpv - dr);  // dS
+      }
+    }
+    const short8_t pf[2] = {pack_frag(pd[0], pd[1]), pack_frag(pd[2], pd[3])};
+    const short8_t sf[2] = {pack_frag(sc[0], sc[1]), pack_frag(sc[2], sc[3])};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      short8_t dof[4], qtf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dof[t] = frag_tr_asm(ds, t, s2, lane);
+        qtf[t] = frag_tr_asm(qs, t, s2, lane);
+      }
+      lds_wait8(dof, qtf);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dv[t] = mfma16(dof[t], pf[s2], dv[t]);
+        dk[t] = mfma16(qtf[t], sf[s2], dk[t]);
+      }
+    }
+    if (i + 1 < nq) wait_tiles(i + 2 < nq ? 1 : 0);
+    gvl_ring::barrier_lds();  // slot st is refilled by iteration i+1's issue
+  }
+  if (kok) {
+    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + key * gg.dk_st;
+    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + key * gg.dv_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(dkr + d) =
+          make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale),
+                     pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
+      *reinterpret_cast<uint2*>(dvr + d) =
+          make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+    }
+  }
+}
+
+// dQ, LDS-DMA pipelined (default for Tq > 64): attn_bwd_dq_kernel with the K / V tiles moved
+// global -> LDS by buffer_load ... lds into a 3-slot ring two key tiles ahead (as
+// attn_bwd_dkdv_dma_kernel; transposed K reads by inline asm for the same reason).
+template <int G, bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG gg) {
+  using gvl_ring::lds_void_t;
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
+  constexpr int QT = 64 * G, SLOT = 2 * KT * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];  // [slot][K, V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Gl = lane >> 4;
+  int64_t qt, h, b;
+  tile_of_block<true>(p, (p.Tq + QT - 1) / QT, qt, h, b);
+  const int64_t qblk0 = qt * QT;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  int64_t q[G];
+  bool qok[G];
+  short8_t qf[G][2], df[G][2];
+  float lse2[G], Dq[G];
+  uint64_t drow[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    qok[g] = q[g] < p.Tq;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qf[g][s2] = load_frag_global(qbase + q[g] * p.q_st, s2, lane, qok[g]);
+      df[g][s2] = load_frag_global(dobase + q[g] * gg.do_st, s2, lane, qok[g]);
+    }
+    const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
+    lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
+    Dq[g] = qok[g] ? gg.Dws[ridx] : 0.f;
+    drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
+  }
+  int64_t kend = p.Tk;
+  if (p.causal) {
+    const int64_t lim = qblk0 + QT;
+    if (lim < kend) kend = lim;
+  }
+  const int nkt = (int)((kend + KT - 1) / KT);
+  float4_t acc[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rk = gvl_ring::uniform_rsrc(kbase, ((p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = gvl_ring::uniform_rsrc(vbase, ((p.Tk - 1) * p.v_st + D) * 2);
+  auto issue = [&](int kt, int slot) {  // 4 DMA instructions per wave
+    char* sb = smem + slot * SLOT;
+    const int64_t k0 = (int64_t)kt * KT;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = 2 * wave + t;
+      const int row = 8 * j + (lane >> 3);
+      const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+      const int vok = (int)(((k0 + row) * p.k_st + chunk * 8) * 2);
+      const int vov = (int)(((k0 + row) * p.v_st + chunk * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void_t*)(sb + j * 1024), 16, vok, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void_t*)(sb + KT * D * 2 + j * 1024), 16,
+                                               vov, 0, 0, 0);
+    }
+  };
+  if (nkt > 0) {
+    issue(0, 0);
+    if (nkt > 1) issue(1, 1);
+    if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    gvl_ring::barrier_lds();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
+    const char* ks = smem + (kt % 3) * SLOT;
+    const char* vs = ks + KT * D * 2;
+    const int64_t k0 = (int64_t)kt * KT;
+    float4_t sc[G][4], dp[G][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+        dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t kf = frag_row(ks, 16 * n, s2, lane);
+        const short8_t vf = frag_row(vs, 16 * n, s2, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          sc[g][n] = mfma16(kf, qf[g][s2], sc[g][n]);
+          dp[g][n] = mfma16(vf, df[g][s2], dp[g][n]);
+        }
+      }
+    }
+    short8_t sf[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
+      const bool msk = k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0);
+      const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kk = 16 * n + 4 * Gl + r;
+          float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lse2[g]));
+          if (msk && (kk >= kl || (p.causal && kk > ql))) pv = 0.f;
+          float dpv = dp[g][n][r];
+          if constexpr (DROP)
+            dpv = rng_keep(seed_, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
+          sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
+        }
+      sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+      sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      short8_t kt4[4], kt4b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kt4[t] = frag_tr_asm(ks, t, s2, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kt4b[t] = kt4[t];
+      lds_wait8(kt4, kt4b);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g][t] = mfma16(kt4[t], sf[g][s2], acc[g][t]);
+    }
+    if (kt + 1 < nkt) {
+      if (kt + 2 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gvl_ring::barrier_lds();
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (!qok[g]) continue;
+    bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + q[g] * gg.dq_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(dst + d) =
+          make_uint2(pack2(acc[g][t][0] * p.scale, acc[g][t][1] * p.scale),
+                     pack2(acc[g][t][2] * p.scale, acc[g][t][3] * p.scale));
     }
   }
 }
@@ -780,7 +1126,15 @@ int fill(const gvl_attn_desc* d, AttnP& p) {
 
 // Two query groups per wave (128-row blocks) only pay off once a block has enough rows;
 // the short caption sequences (31-64 rows) keep 64-row blocks.
-int pick_groups(int64_t T) { return T > 64 ? 2 : 1; }
+// GVL_ATTN_G=1 keeps 64-row blocks everywhere (A/B of occupancy against rows per block).
+int pick_groups(int64_t T) {
+  static const int forced = [] {
+    const char* e = getenv("GVL_ATTN_G");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1) return 1;
+  return T > 64 ? 2 : 1;
+}
 
 // dK/dV key groups per wave: GVL_DKDV_G=2 runs 32 keys per wave (one wave per SIMD, the
 // accumulators need > 256 registers) for Tk > 64; default 1.
@@ -798,6 +1152,24 @@ bool short_bwd_enabled() {
   static const bool on = [] {
     const char* e = getenv("GVL_ATTN_SHORT");
     return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// LDS-DMA pipelined dQ and dK/dV (attn_bwd_dq_dma_kernel, attn_bwd_dkdv_dma_kernel);
+// GVL_DKDV_DMA=0 restores the register-staged kernels (A/B).
+bool dkdv_dma_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_DKDV_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool dq_dma_enabled() {  // GVL_DQ_DMA=0: register-staged dQ kernel beside the DMA dK/dV one
+  static const bool on = [] {
+    const char* e = getenv("GVL_DQ_DMA");
+    return dkdv_dma_enabled() && !(e && e[0] == '0');
   }();
   return on;
 }
@@ -860,7 +1232,15 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
   const int Gq = pick_groups(d->Tq);
   dim3 gq(grid_1d(d, (d->Tq + 64 * Gq - 1) / (64 * Gq)));
-  if (Gq == 2) {
+  if (dq_dma_enabled()) {
+    if (Gq == 2) {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<2, true>, gq, dim3(NT), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_dq_dma_kernel<2, false>, gq, dim3(NT), 0, s, p, g);
+    } else {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<1, true>, gq, dim3(NT), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_dq_dma_kernel<1, false>, gq, dim3(NT), 0, s, p, g);
+    }
+  } else if (Gq == 2) {
     if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), gq, dim3(NT), 0, s, p, g);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), gq, dim3(NT), 0, s, p, g);
   } else {
@@ -872,7 +1252,10 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   // accumulators for 32 keys x 64 dims) and spill to scratch.
   const int Gk = dkdv_groups(d->Tk);
   dim3 gk(grid_1d(d, (d->Tk + 64 * Gk - 1) / (64 * Gk)));
-  if (Gk == 2) {
+  if (Gk == 1 && dkdv_dma_enabled()) {
+    if (p.has_drop) gvl::launch_timed(attn_bwd_dkdv_dma_kernel<true>, gk, dim3(NT), 0, s, p, g);
+    else gvl::launch_timed(attn_bwd_dkdv_dma_kernel<false>, gk, dim3(NT), 0, s, p, g);
+  } else if (Gk == 2) {
     if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), gk, dim3(NT), 0, s, p, g);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), gk, dim3(NT), 0, s, p, g);
   } else {
