@@ -208,7 +208,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 9, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 10, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -225,9 +225,12 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
       snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
+    } else if ((env().cfg < 0 || env().cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, env().cfg == 10)) {
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
+      snprintf(buf, len, "gemm_w4_kernel<3, %s, %s>", tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
     } else if (env().cfg >= 0) {
-      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg), tf[d->a_mn != 0],
-               tf[d->b_mn != 0]);
+      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg == 10 ? 3 : env().cfg),
+               tf[d->a_mn != 0], tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
@@ -274,8 +277,11 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
-    if (env().cfg >= 0) {
-      gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg, s);
+    if (env().cfg == 10 && gvl::gemm_w4_plan(p, d->a_mn, true)) {
+      gvl::gemm_w4_launch(p, d->b_mn, s);
+    } else if (env().cfg >= 0) {
+      gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg == 10 ? 3 : env().cfg, s);
+    } else if (gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
     } else if (env().impl == 4 && gvl::gemm_8p_try(p, d->a_mn, d->b_mn, false, s)) {
     } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
       gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn), s);

@@ -468,4 +468,7 @@ int gemm_pp3_launch_tt(const GemmP& p, hipStream_t s);
 int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
 bool gemm_8p_plan(GemmP& p, bool force);
 bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
+bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
+int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
+bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 }  // namespace gvl

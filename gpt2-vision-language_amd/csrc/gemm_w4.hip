@@ -1,0 +1,273 @@
+// Four-wave deep-ring GEMM for narrow outputs (N = 768 at M = 8064: the caption decoder's
+// attn.c_proj / mlp.c_proj forward and c_attn / c_fc / c_proj dX).
+//
+// Why a fourth kernel: those outputs are 96 tiles of 256x256 (a third of the chip) or 378 of
+// 128x128 (1.5 rounds), and the 192x128 tile that fills the chip in one round (42 x 6 = 252
+// tiles at M = 8064) ran no faster than 128x128 in the ring kernel (gemm_ring.hip cfg 7): with
+// one workgroup of 4 waves per CU there is one wave per SIMD, so every stall is an MFMA bubble,
+// and its 4-slot ring keeps only two 32-deep K-steps (~0.35 us of MFMA work) in flight — less
+// than an L2/MALL miss.  Here:
+//   * tile 192x128, 4 waves of 96x64 (6 x 4 fragments, 24 MFMA 16x16x32 per K-step);
+//   * an NS-slot LDS-DMA ring (7 x 20 KiB = 140 KiB): NS - 2 K-steps stay in flight past
+//     every barrier (~1 us of MFMA work), one barrier per K-step, counted vmcnt waits;
+//   * fragments double-buffered in registers: the 10 ds_reads of step c+1 are issued before
+//     the 24 MFMAs of step c, so the LDS latency hides behind them;
+//   * persistent over tiles (grid = min(tiles, CUs)) with the ring running across tile
+//     boundaries, XCD-contiguous + L2-grouped tile walk, compile-time fused epilogues with
+//     16-B stores (gemm_epilogue16, as gemm_pp3_kernel).
+// A must be K-contiguous (activations / output gradients); B either layout (nn.Linear weight
+// in the forward, the same weight MN-contiguous in dX).  K % 64 == 0.
+#include "common.h"
+#include "capi_util.h"
+#include "gemm_common.h"
+#include "gemm_ring.h"
+#include "../../include/gvl.h"
+
+namespace {
+
+using namespace gvl_ring;
+
+constexpr int W4_BM = 192, W4_BN = 128;
+
+// Register-staged operand copy of one K-step: this wave's PER 1-KiB pieces (the Step images,
+// swizzle on the global source address) loaded to VGPRs, later written lane-linear to LDS.
+// (LDS-DMA would need no VGPRs, but each buffer_load...lds costs ~60-185 issue cycles at one
+// wave per SIMD, MICROARCH cycle constants: 5 pieces per K-step ~ the whole MFMA budget.)
+template <int PER>
+GVL_DEV void w4_load(__amdgpu_buffer_rsrc_t rs, const int* off, int kbytes, uint4* v) {
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    v[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[t], kbytes, 0));
+}
+template <int PER, int NWV>
+GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    *reinterpret_cast<uint4*>(lds + (t * NWV + wave) * 1024 + lane * 16) = v[t];
+}
+
+// K-steps are 32 deep; the register staging runs P = 3 steps ahead of the LDS writes, the LDS
+// ring holds NS = 3 steps (the one being read, the next, the one being written).  Step c:
+//   read the fragments of step c+1 (written and published by the previous barrier);
+//   write step c+2 from its register set to LDS slot (c+2)%3 (slot of step c-1, whose reads
+//   retired before the previous barrier), then reload that set with step c+5;
+//   MFMAs of step c; barrier (retires this step's fragment reads and LDS writes).
+// The loop body is unrolled 6 times (register set = step % 3, fragment buffer = step % 2, both
+// static), so K must be a multiple of 6 steps (K % 192 == 0).
+template <int NS, bool BMN, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
+  constexpr int BM = W4_BM, BN = W4_BN, NW = 4, FM = 6, FN = 4, P = 3;
+  static_assert(NS == 3, "ring geometry");
+  using SA = Step<BM, false, NW>;
+  using SB = Step<BN, BMN, NW>;
+  constexpr int SLOT = SA::BYTES + SB::BYTES;
+  constexpr int PA = SA::PER, PB = SB::PER;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int arow = (wave >> 1) * (BM / 2), bcol = (wave & 1) * (BN / 2);
+
+  const int total = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int ntl = (total - b + G - 1) / G;
+  const int nks = (int)(p.K / KS);
+  const int nsteps = ntl * nks;
+  auto tile_coords = [&](int t, int64_t& m0, int64_t& n0) {
+    const int vid = b + t * G;
+    const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
+    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
+    int sp, tm, tn;
+    gemm_tile_of(work, 1, p.tiles_m, p.tiles_n, p.group, sp, tm, tn);
+    m0 = (int64_t)tm * BM;
+    n0 = (int64_t)tn * BN;
+  };
+
+  const int64_t b_rows = BMN ? p.K : p.N;
+  const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, p.M * p.lda * 2);
+  const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
+  const int sa_step = SA::step_bytes(p.lda), sb_step = SB::step_bytes(p.ldb);
+  int is_t = 0, is_k = 0;  // load cursor (steps are loaded strictly in order)
+  int offa[PA], offb[PB];
+  {
+    int64_t m0, n0;
+    tile_coords(0, m0, n0);
+    SA::base_offsets(p.lda, m0, 0, wave, lane, offa);
+    SB::base_offsets(p.ldb, n0, 0, wave, lane, offb);
+  }
+  uint4 st[P][PA + PB];
+// Loads and LDS writes past the last step are issued anyway (they re-read the last tile's
+// first steps into a slot nobody reads again): a branch around them would make hipcc's
+// vmcnt bookkeeping assume the newest loads belong to the set being written and wait for
+// all of them (no loads left in flight).
+#define GVL_W4_LOAD(SET)                                                        \
+  do {                                                                          \
+    w4_load<PA>(ra, offa, is_k * sa_step, st[SET]);                             \
+    w4_load<PB>(rb, offb, is_k * sb_step, st[SET] + PA);                        \
+    if (++is_k == nks) {                                                        \
+      is_k = 0;                                                                 \
+      if (++is_t < ntl) {                                                       \
+        int64_t m0_, n0_;                                                       \
+        tile_coords(is_t, m0_, n0_);                                            \
+        SA::base_offsets(p.lda, m0_, 0, wave, lane, offa);                      \
+        SB::base_offsets(p.ldb, n0_, 0, wave, lane, offb);                      \
+      }                                                                         \
+    }                                                                           \
+  } while (0)
+#define GVL_W4_WRITE(C, SET)  /* step C lives in LDS slot C % 3 == SET */     \
+  do {                                                                          \
+    char* slot_ = smem + (SET) * SLOT;                                          \
+    w4_store<PA, NW>(slot_, st[SET], wave, lane);                               \
+    w4_store<PB, NW>(slot_ + SA::BYTES, st[SET] + PA, wave, lane);              \
+  } while (0)
+
+  float4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  int64_t cu_m0, cu_n0;
+  tile_coords(0, cu_m0, cu_n0);
+  EpiPre<FM, FN, EPI> pre;
+  pre.load_bias(p, cu_n0 + bcol, lane);
+
+  // prologue: steps 0..2 into sets 0..2; steps 0, 1 written; sets 0, 1 reloaded with 3, 4
+  GVL_W4_LOAD(0);
+  GVL_W4_LOAD(1);
+  GVL_W4_LOAD(2);
+  GVL_W4_WRITE(0, 0);
+  GVL_W4_LOAD(0);
+  GVL_W4_WRITE(1, 1);
+  GVL_W4_LOAD(1);
+  barrier_lds();
+  short8_t af[FM], bf[FN], an[FM], bn[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bf[j] = SB::frag(smem + SA::BYTES, bcol + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) af[i] = SA::frag(smem, arow + 16 * i, lane);
+
+#define GVL_W4_STEP(C, SET, CA, CB, NA, NB)                                                 \
+  do {                                                                                      \
+    { /* step C+1 in slot (SET + 2) % 3 */                                                  \
+      const char* sl_ = smem + (((SET) + 2) % 3) * SLOT;                                    \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
+          NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                           \
+      _Pragma("unroll") for (int i = 0; i < FM; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
+    }                                                                                       \
+    GVL_W4_WRITE((C) + 2, SET);                                                             \
+    GVL_W4_LOAD(SET);                                                                       \
+    __builtin_amdgcn_s_setprio(1);                                                          \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                          \
+        _Pragma("unroll") for (int j = 0; j < FN; ++j)                                      \
+            acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]);                                    \
+    __builtin_amdgcn_s_setprio(0);                                                          \
+    barrier_lds();                                                                          \
+  } while (0)
+
+  int c = 0;
+  for (int t = 0; t < ntl; ++t) {
+    for (int k = 0; k < nks; k += 6, c += 6) {
+      GVL_W4_STEP(c, 2, af, bf, an, bn);
+      GVL_W4_STEP(c + 1, 0, an, bn, af, bf);
+      GVL_W4_STEP(c + 2, 1, af, bf, an, bn);
+      GVL_W4_STEP(c + 3, 2, an, bn, af, bf);
+      GVL_W4_STEP(c + 4, 0, af, bf, an, bn);
+      GVL_W4_STEP(c + 5, 1, an, bn, af, bf);
+    }
+    gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    if (t + 1 < ntl) {
+      tile_coords(t + 1, cu_m0, cu_n0);
+      pre.load_bias(p, cu_n0 + bcol, lane);
+    }
+  }
+#undef GVL_W4_STEP
+#undef GVL_W4_WRITE
+#undef GVL_W4_LOAD
+}
+
+#ifndef GVL_W4_NS
+#define GVL_W4_NS 3
+#endif
+
+template <bool BMN, int EPI>
+int launch_w4(const GemmP& p0, hipStream_t s) {
+  constexpr int NS = GVL_W4_NS;
+  GemmP p = p0;
+  p.tiles_m = (int)((p.M + W4_BM - 1) / W4_BM);
+  p.tiles_n = (int)((p.N + W4_BN - 1) / W4_BN);
+  p.splits = 1;
+  p.kper = p.K;
+  constexpr int lds = NS * (W4_BM + W4_BN) * KS * 2;
+  auto kern = gemm_w4_kernel<GVL_W4_NS, BMN, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  const int total = p.tiles_m * p.tiles_n;
+  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
+  gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
+  return 0;
+}
+
+template <bool BMN>
+int launch_w4_epi(const GemmP& p, hipStream_t s) {
+  switch (gvl::gemm_epi_kind(p)) {
+    case EPI_PLAIN: return launch_w4<BMN, EPI_PLAIN>(p, s);
+    case EPI_BIAS: return launch_w4<BMN, EPI_BIAS>(p, s);
+    case EPI_BIAS_RES: return launch_w4<BMN, EPI_BIAS_RES>(p, s);
+    case EPI_BIAS_ACT: return launch_w4<BMN, EPI_BIAS_ACT>(p, s);
+    case EPI_DACT: return launch_w4<BMN, EPI_DACT>(p, s);
+    case EPI_RES: return launch_w4<BMN, EPI_RES>(p, s);
+    case EPI_BIAS_ACT_ERF: return launch_w4<BMN, EPI_BIAS_ACT_ERF>(p, s);
+    case EPI_DACT_ERF: return launch_w4<BMN, EPI_DACT_ERF>(p, s);
+    case EPI_BIAS_ACT_D: return launch_w4<BMN, EPI_BIAS_ACT_D>(p, s);
+    case EPI_BIAS_ACT_ERF_D: return launch_w4<BMN, EPI_BIAS_ACT_ERF_D>(p, s);
+    case EPI_MUL: return launch_w4<BMN, EPI_MUL>(p, s);
+    default: return -1;
+  }
+}
+
+// Routing: GVL_W4=0 disables, =2 forces it for every shape it supports (tests / A/B).
+int w4_mode() {
+  static const int v = [] {
+    const char* e = getenv("GVL_W4");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+}  // namespace
+
+namespace gvl {
+
+// Shapes it takes by default: narrow outputs (N <= 1024) whose 256x256 tiling leaves most CUs
+// idle and whose 192x128 tiling fills at least half the chip.
+bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
+  if (a_mn || p.c_f32 || p.K % (6 * KS) != 0 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
+  if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
+  if (gemm_epi_kind(p) == EPI_GEN) return false;
+  if (force || w4_mode() == 2) return true;
+  if (w4_mode() == 0) return false;
+  const int64_t cus = num_cus();
+  const int64_t t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const int64_t tw4 = ((p.M + W4_BM - 1) / W4_BM) * ((p.N + W4_BN - 1) / W4_BN);
+  return p.N <= 1024 && t256 < 160 && tw4 * 2 >= cus && tw4 <= cus;
+}
+
+int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
+  return b_mn ? launch_w4_epi<true>(p, s) : launch_w4_epi<false>(p, s);
+}
+
+bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s) {
+  if (!gemm_w4_plan(p, a_mn, false)) return false;
+  return gemm_w4_launch(p, b_mn, s) == 0;
+}
+
+}  // namespace gvl

@@ -299,7 +299,10 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
     name = _kernel_name(A, B, a_mn, b_mn, M, N, K)
-    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
+    if not a_mn and K % 192 == 0:  # K-contiguous A: the four-wave 192x128 kernel takes it
+        assert name.startswith("gemm_w4_kernel"), name
+    else:
+        assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
@@ -324,6 +327,60 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
         O.gelu_tanh(hx).sum().backward()
         kw, ref = dict(dact=1, pre_in=hpre.to(cuda)), h * hx.grad
     y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
+    if epi == "bias_act_d":
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("b_mn", [0, 1])
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "res_inplace", "bias_act_d", "mul", "dact_erf"])
+@pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 2304), (7992, 776, 192),
+                                   (16384, 768, 384), (300, 128, 192)])
+def test_gemm_w4(cuda, b_mn, epi, M, N, K):
+    """Four-wave 192x128 deep-ring kernel (gemm_w4.hip), forced with gvl_gemm_tune(3, 10):
+    the caption decoder's N = 768 shapes (252 tiles, one per CU), ragged M and N (N % 128 != 0),
+    several tiles per workgroup with the ring running across tiles (516 tiles), a tile grid
+    smaller than the ring, and every epilogue kind."""
+    from gvl import _lib
+    K_ = _k()
+    torch.manual_seed(M + N + K + len(epi) + 7 * b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = a.to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    h = a.float() @ b.float()
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    kw, ref = {}, h
+    if epi == "bias":
+        kw, ref = dict(bias=bias.to(cuda)), h + bias.float()
+    elif epi == "bias_res":
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    elif epi == "res_inplace":
+        acc = res.to(cuda)
+        kw, ref = dict(residual=acc, out=acc), h + res.float()
+    elif epi == "bias_act_d":
+        x = (h + bias.float()).requires_grad_(True)
+        g = O.gelu_tanh(x)
+        g.sum().backward()
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=3, pre_out=pre), g.detach()
+    elif epi == "mul":
+        d = torch.randn(M, N).to(BF)
+        kw, ref = dict(dact=3, pre_in=d.to(cuda)), h * d.float()
+    elif epi == "dact_erf":
+        hpre = torch.randn(M, N).to(BF)
+        hx = hpre.float().requires_grad_(True)
+        O.gelu_erf(hx).sum().backward()
+        kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
+    _lib.lib().gvl_gemm_tune(3, 10)
+    try:
+        name = _kernel_name(A, B, 0, b_mn, M, N, K)
+        y = K_.gemm(A, B, a_mn=False, b_mn=bool(b_mn), **kw)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+    assert name.startswith("gemm_w4_kernel"), name
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
