@@ -54,6 +54,69 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
 //   MFMAs of step c; barrier (retires this step's fragment reads and LDS writes).
 // The loop body is unrolled 6 times (register set = step % 3, fragment buffer = step % 2, both
 // static), so K must be a multiple of 6 steps (K % 192 == 0).
+// GVL_W4_IGLP (default 3, measured best of 0-3 on the caption shapes; 0 = off): ask the scheduler to spread the step's LDS reads, LDS writes and global
+// loads between its 24 MFMAs (one wave per SIMD: whatever is not issued in an MFMA's shadow
+// is an MFMA bubble) instead of issuing them as one block ahead of the MFMAs.
+#ifndef GVL_W4_IGLP
+#define GVL_W4_IGLP 3
+#endif
+#if GVL_W4_IGLP == 1  // reads, then writes, then global loads, one per MFMA
+#define W4_INTERLEAVE()                                                           \
+  do {                                                                            \
+    _Pragma("unroll") for (int q_ = 0; q_ < 10; ++q_) {                           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
+    }                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                          \
+    }                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                          \
+    }                                                                             \
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
+  } while (0)
+#elif GVL_W4_IGLP == 2  // global loads first, then reads, then writes
+#define W4_INTERLEAVE()                                                           \
+  do {                                                                            \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                          \
+    }                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < 10; ++q_) {                           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
+    }                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                          \
+    }                                                                             \
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
+  } while (0)
+#elif GVL_W4_IGLP == 3  // five rounds of {MFMA, read, MFMA, read, MFMA, load, MFMA, write}
+#define W4_INTERLEAVE()                                                           \
+  do {                                                                            \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                          \
+    }                                                                             \
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
+  } while (0)
+#endif
+#if GVL_W4_IGLP
+#define W4_PRIO(x) do {} while (0)  // s_setprio would split the scheduling region
+#else
+#define W4_INTERLEAVE() do {} while (0)
+#define W4_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#endif
+
 template <int NS, bool BMN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
   constexpr int BM = W4_BM, BN = W4_BN, NW = 4, FM = 6, FN = 4, P = 3;
@@ -71,7 +134,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
   const int G = gridDim.x, b = blockIdx.x;
   const int ntl = (total - b + G - 1) / G;
   const int nks = (int)(p.K / KS);
-  const int nsteps = ntl * nks;
   auto tile_coords = [&](int t, int64_t& m0, int64_t& n0) {
     const int vid = b + t * G;
     const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
@@ -158,11 +220,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
     }                                                                                       \
     GVL_W4_WRITE((C) + 2, SET);                                                             \
     GVL_W4_LOAD(SET);                                                                       \
-    __builtin_amdgcn_s_setprio(1);                                                          \
+    W4_PRIO(1);                                                                             \
     _Pragma("unroll") for (int i = 0; i < FM; ++i)                                          \
         _Pragma("unroll") for (int j = 0; j < FN; ++j)                                      \
             acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]);                                    \
-    __builtin_amdgcn_s_setprio(0);                                                          \
+    W4_PRIO(0);                                                                             \
+    W4_INTERLEAVE();                                                                        \
     barrier_lds();                                                                          \
   } while (0)
 
