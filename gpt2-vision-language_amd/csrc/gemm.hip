@@ -222,17 +222,17 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     fill_params(d, p);
     GemmP q = p;
     if (env().impl == 4 && env().cfg < 0 && gvl::gemm_8p_plan(q, false)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
     } else if ((env().cfg < 0 || env().cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, env().cfg == 10)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       snprintf(buf, len, "gemm_w4_kernel<3, %s, %s>", tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
     } else if (env().cfg >= 0) {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg == 10 ? 3 : env().cfg),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm);

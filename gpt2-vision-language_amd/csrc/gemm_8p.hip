@@ -325,7 +325,7 @@ namespace gvl {
 bool gemm_8p_plan(GemmP& p, bool force) {
   if (p.K % BK != 0) return false;
   if (!gemm_pp3_plan(p, force, BK)) return false;
-  return gemm_epi_kind(p) != EPI_GEN;
+  return gemm_epi_kind(p) != EPI_GEN && gemm_epi_kind(p) != EPI_BIAS_DROP_RES;
 }
 
 bool gemm_8p_try(const GemmP& p0, int a_mn, int b_mn, bool force, hipStream_t s) {

@@ -169,9 +169,12 @@ enum {
   EPI_RES = 6,  // C = AB + residual (in-place gradient accumulation: residual == C)
   EPI_BIAS_ACT_ERF = 7, EPI_DACT_ERF = 8,  // 3 / 4 are the tanh-GELU forms
   // GELU forward storing gelu'(x) (act 3 / 4) and the backward multiply by it (dact 3)
-  EPI_BIAS_ACT_D = 9, EPI_BIAS_ACT_ERF_D = 10, EPI_MUL = 11
+  EPI_BIAS_ACT_D = 9, EPI_BIAS_ACT_ERF_D = 10, EPI_MUL = 11,
+  // C = residual + dropout(AB + bias): the Q-Former out_proj / MLP output branches
+  // (gpt2_q_former/model.py:139-145, q += drop(...)), mask = the counter hash of (m, n)
+  EPI_BIAS_DROP_RES = 12
 };
-constexpr int EPI_KINDS = 12;
+constexpr int EPI_KINDS = 13;
 
 template <int EPI>
 struct EpiKind {
@@ -180,8 +183,9 @@ struct EpiKind {
   static constexpr bool MUL = EPI == EPI_MUL;
   static constexpr bool DACT = EPI == EPI_DACT || EPI == EPI_DACT_ERF || MUL;
   static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF || EPI == EPI_BIAS_ACT_ERF_D;
-  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT;
-  static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES;
+  static constexpr bool DROP = EPI == EPI_BIAS_DROP_RES;
+  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT || DROP;
+  static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES || DROP;
   static constexpr bool AUX = DACT || RES;  // reads a bf16 [M, N] operand (pre_in / residual)
 };
 
@@ -198,7 +202,9 @@ struct EpiPre {
   uint2 b[KD::BIAS ? FN : 1];
   static constexpr int XH = FM / 2;  // the [M, N] operand is fetched half a tile at a time
   uint2 x[KD::AUX ? XH : 1][KD::AUX ? FN : 1];
+  uint64_t seed = 0;  // effective dropout seed (DROP), read with the bias, not per element
   GVL_DEV void load_bias(const GemmP& p, int64_t nw0, int lane) {
+    if constexpr (KD::DROP) seed = seed_eff(p.seed, p.seed_ptr);
     if constexpr (KD::BIAS) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -230,7 +236,8 @@ template <int EPI>
 static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t a, int64_t m,
                                                           int64_t n, float alpha, float gatev,
                                                           const uint2& bb, const uint2& ax,
-                                                          float (&v)[4], float (&pre)[4]) {
+                                                          float (&v)[4], float (&pre)[4],
+                                                          uint64_t seed = 0) {
   if constexpr (EPI == EPI_GEN) {
     gemm_epi_vals(p, a, m, n, alpha, gatev, v);
   } else {
@@ -257,6 +264,12 @@ static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t 
           v[r] = KD::ERF ? gelu_erf(v[r]) : gelu_tanh(v[r]);
         }
       }
+    }
+    if constexpr (KD::DROP) {
+      const uint64_t base = (uint64_t)m * (uint64_t)p.N + (uint64_t)n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[r] = rng_keep(seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
     }
     if constexpr (KD::RES) {
       v[0] += lo_bf(ax.x); v[1] += hi_bf(ax.x); v[2] += lo_bf(ax.y); v[3] += hi_bf(ax.y);
@@ -315,8 +328,8 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         constexpr int XH = EpiPre<FM, FN, EPI>::XH;
         const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
         const uint2 a1 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j + 1 : 0] : make_uint2(0, 0);
-        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0);
-        if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, b1, a1, v1, h1);
+        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0, pre.seed);
+        if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, b1, a1, v1, h1, pre.seed);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
         x1 = pack2(v1[0], v1[1]); y1 = pack2(v1[2], v1[3]);
         if (KD::ACT && p.pre_out) {  // pre-activation: same lane swap, 16-B stores
@@ -349,7 +362,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         const uint2 b0 = KD::BIAS ? pre.b[KD::BIAS ? j : 0] : make_uint2(0, 0);
         constexpr int XH = EpiPre<FM, FN, EPI>::XH;
         const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
-        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0);
+        if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0, pre.seed);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
         if (KD::ACT && p.pre_out && mok && n0 < p.N)
           *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n0) =

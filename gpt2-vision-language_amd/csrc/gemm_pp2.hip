@@ -178,6 +178,8 @@ const char* gemm_pp2_name(int cfg) {
 }
 
 int gemm_epi_kind(const GemmP& p) {
+  if (p.has_drop && !p.gate && !p.c_f32 && !p.act && !p.dact && p.bias && p.residual)
+    return EPI_BIAS_DROP_RES;
   if (p.has_drop || p.gate || p.c_f32) return EPI_GEN;
   const bool b = p.bias != nullptr, r = p.residual != nullptr;
   if (!p.act && !p.dact) {

@@ -293,6 +293,7 @@ int launch_w4_epi(const GemmP& p, hipStream_t s) {
     case EPI_BIAS_ACT_D: return launch_w4<BMN, EPI_BIAS_ACT_D>(p, s);
     case EPI_BIAS_ACT_ERF_D: return launch_w4<BMN, EPI_BIAS_ACT_ERF_D>(p, s);
     case EPI_MUL: return launch_w4<BMN, EPI_MUL>(p, s);
+    case EPI_BIAS_DROP_RES: return launch_w4<BMN, EPI_BIAS_DROP_RES>(p, s);
     default: return -1;
   }
 }

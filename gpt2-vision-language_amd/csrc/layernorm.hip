@@ -91,8 +91,8 @@ template <int IT>
 __global__ __launch_bounds__(LN_BWD_NT) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
-    const float* __restrict__ rstd_in, bf16_t* __restrict__ dx, int64_t lddx, int acc_dx,
-    float* __restrict__ ws, int64_t rows, int C) {
+    const float* __restrict__ rstd_in, const bf16_t* res, int64_t ldr, bf16_t* dx, int64_t lddx,
+    int acc_dx, float* __restrict__ ws, int64_t rows, int C) {
   __shared__ float red[LN_BWD_NT / 64][2 * 64 * 4 * IT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float pw[IT][4], pb[IT][4];
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(LN_BWD_NT) void ln_bwd_kernel(
       if (c < C) {
         xu[it] = *reinterpret_cast<const uint2*>(x + r * ldx + c);
         du[it] = *reinterpret_cast<const uint2*>(dy + r * lddy + c);
-        if (acc_dx) pu[it] = *reinterpret_cast<const uint2*>(dx + r * lddx + c);
+        if (acc_dx) pu[it] = *reinterpret_cast<const uint2*>(res + r * ldr + c);
       }
     }
   };
@@ -268,13 +268,14 @@ extern "C" int64_t gvl_layernorm_bwd_workspace_size(int64_t rows, int64_t cols) 
   return (int64_t)ln_bwd_blocks(rows) * 2 * cols * (int64_t)sizeof(float);
 }
 
-extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx,
-                                 const void* w, const float* mean, const float* rstd, void* dx,
-                                 int64_t lddx, int32_t accumulate_dx, void* dw, void* db,
-                                 int32_t accumulate_wb, void* workspace, int64_t rows, int64_t cols,
-                                 gvl_stream_t stream) {
+// dx = [res +] LN backward; res may alias dx (in-place accumulation, gvl_layernorm_bwd)
+static int ln_bwd_launch(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
+                         const float* mean, const float* rstd, const void* res, int64_t ldr,
+                         void* dx, int64_t lddx, int32_t accumulate_dx, void* dw, void* db,
+                         int32_t accumulate_wb, void* workspace, int64_t rows, int64_t cols,
+                         gvl_stream_t stream) {
   GVL_REQUIRE(ln_shape_ok(cols, lddy, ldx, dy, x) && lddx % 8 == 0 && gvl::aligned16(dx) &&
-                  gvl::aligned16(w),
+                  gvl::aligned16(w) && (!accumulate_dx || (ldr % 8 == 0 && gvl::aligned16(res))),
               "gvl_layernorm_bwd: cols unsupported (need cols %% 8 == 0, <= 1024, ld %% 8 == 0, "
               "16-byte aligned rows)");
   GVL_REQUIRE(!(dw || db) || workspace, "gvl_layernorm_bwd: dw/db need a workspace");
@@ -285,13 +286,14 @@ extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
   const auto dyp = static_cast<const bf16_t*>(dy);
   const auto xp = static_cast<const bf16_t*>(x);
   const auto wp = static_cast<const bf16_t*>(w);
+  const auto rp = static_cast<const bf16_t*>(res);
   auto dxp = static_cast<bf16_t*>(dx);
   if (cols <= 768)
     hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(LN_BWD_NT), 0, s, dyp, lddy, xp, ldx, wp,
-                       mean, rstd, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
+                       mean, rstd, rp, ldr, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(LN_BWD_NT), 0, s, dyp, lddy, xp, ldx, wp,
-                       mean, rstd, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
+                       mean, rstd, rp, ldr, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd");
   if (ws) {
     const int g2 = (int)((2 * cols + 15) / 16);
@@ -300,4 +302,23 @@ extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
     GVL_LAUNCH_CHECK("gvl_layernorm_bwd(finalize)");
   }
   return 0;
+}
+
+extern "C" int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                                 const void* w, const float* mean, const float* rstd, void* dx,
+                                 int64_t lddx, int32_t accumulate_dx, void* dw, void* db,
+                                 int32_t accumulate_wb, void* workspace, int64_t rows, int64_t cols,
+                                 gvl_stream_t stream) {
+  return ln_bwd_launch(dy, lddy, x, ldx, w, mean, rstd, dx, lddx, dx, lddx, accumulate_dx, dw, db,
+                       accumulate_wb, workspace, rows, cols, stream);
+}
+
+extern "C" int gvl_layernorm_bwd_res(const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                                     const void* w, const float* mean, const float* rstd,
+                                     const void* res, int64_t ldr, void* dx, int64_t lddx, void* dw,
+                                     void* db, int32_t accumulate_wb, void* workspace, int64_t rows,
+                                     int64_t cols, gvl_stream_t stream) {
+  GVL_REQUIRE(res != nullptr, "gvl_layernorm_bwd_res: null residual");
+  return ln_bwd_launch(dy, lddy, x, ldx, w, mean, rstd, res, ldr, dx, lddx, 1, dw, db,
+                       accumulate_wb, workspace, rows, cols, stream);
 }

@@ -77,6 +77,8 @@ SIGNATURES = {
     "gvl_layernorm_bwd_workspace_size": (c_i64, [c_i64, c_i64]),
     "gvl_layernorm_bwd": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
                                     c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp]),
+    "gvl_layernorm_bwd_res": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                        c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp]),
     "gvl_attn_fwd": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
     "gvl_attn_bwd_workspace_size": (c_i64, [C.POINTER(AttnDesc)]),
     "gvl_attn_bwd": (C.c_int, [C.POINTER(AttnDesc), C.POINTER(AttnBwdDesc), c_vp]),

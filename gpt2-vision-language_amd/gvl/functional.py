@@ -156,14 +156,15 @@ def _bgrad(ctx, i, p, dy2):
     return None
 
 
-def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx):
-    """LayerNorm backward writing/accumulating dx; returns the (dw, db) autograd outputs."""
+def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx, residual=None):
+    """LayerNorm backward writing/accumulating dx (or dx = residual + ..., no copy of the
+    residual gradient); returns the (dw, db) autograd outputs."""
     nw, nb = _need(ctx, iw), _need(ctx, ib)
     gw = _sink(w, ctx) if nw else None
     gb = _sink(b, ctx) if nb else None
     if (nw or nb) and (gw is not None or not nw) and (gb is not None or not nb):
         K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=gw, db=gb,
-                        accumulate_wb=True)
+                        accumulate_wb=True, residual=residual)
         for p, n in ((w, nw), (b, nb)):
             if n:
                 _ready(p)
@@ -171,7 +172,8 @@ def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx):
     C = x2.shape[1]
     dw = torch.empty(C, dtype=BF16, device=x2.device) if nw else None
     db = torch.empty(C, dtype=BF16, device=x2.device) if nb else None
-    K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=dw, db=db)
+    K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=dw, db=db,
+                    residual=residual)
     return dw, db
 
 
@@ -229,8 +231,8 @@ class GPTBlockFn(torch.autograd.Function):
         g[9] = _wgrad(ctx, 9, P[9], dpre, xn2)
         g[10] = _bgrad(ctx, 10, P[10], dpre)
         dxn2 = K.linear_dx(dpre, fc_w)
-        dxm = d2.clone()
-        g[7], g[8] = _ln_bwd(ctx, 7, 8, P[7], P[8], dxn2, xm, m2, r2, dxm, True)
+        dxm = torch.empty_like(d2)  # = d2 + LN_2 backward (the residual read from d2, no copy)
+        g[7], g[8] = _ln_bwd(ctx, 7, 8, P[7], P[8], dxn2, xm, m2, r2, dxm, True, residual=d2)
         # attention c_proj
         g[5] = _wgrad(ctx, 5, P[5], dxm, y.view(B * T, C))
         g[6] = _bgrad(ctx, 6, P[6], dxm)
@@ -532,8 +534,8 @@ class CrossAttnFn(torch.autograd.Function):
         if _need(ctx, 1):
             g[1] = K.linear_dx(dkvp, kv_w).view(B, S, C)
         dxn = K.linear_dx(dqp, q_w)
-        dx = d2.clone()
-        g[2], g[3] = _ln_bwd(ctx, 2, 3, P[2], P[3], dxn, x2, mean, rstd, dx, True)
+        dx = torch.empty_like(d2)  # = d2 + LN backward (residual read from d2, no copy)
+        g[2], g[3] = _ln_bwd(ctx, 2, 3, P[2], P[3], dxn, x2, mean, rstd, dx, True, residual=d2)
         g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
         return tuple(g)
 

@@ -228,7 +228,9 @@ def layernorm_fwd(x2, w, b, eps=1e-5, out=None, stats=True):
 
 
 def layernorm_bwd(dy2, x2, w, mean, rstd, dx=None, accumulate_dx=False, dw=None, db=None,
-                  accumulate_wb=False):
+                  accumulate_wb=False, residual=None):
+    """dx [= dx | residual] + LayerNorm backward; `residual` (a [rows, cols] bf16 operand read
+    instead of dx, gvl_layernorm_bwd_res) saves the caller a copy of the residual gradient."""
     rows, cols = x2.shape
     if dx is None:
         dx = torch.empty(rows, cols, dtype=BF16, device=x2.device)
@@ -236,6 +238,13 @@ def layernorm_bwd(dy2, x2, w, mean, rstd, dx=None, accumulate_dx=False, dw=None,
     if dw is not None or db is not None:
         n = _L().gvl_layernorm_bwd_workspace_size(rows, cols)
         ws = torch.empty(max(n, 4) // 4, dtype=F32, device=x2.device)
+    if residual is not None:
+        _lib.check(_L().gvl_layernorm_bwd_res(
+            dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
+            mean.data_ptr(), rstd.data_ptr(), residual.data_ptr(), residual.stride(0),
+            dx.data_ptr(), dx.stride(0), _p(dw), _p(db), int(accumulate_wb), _p(ws), rows, cols,
+            _stream()), "gvl_layernorm_bwd_res")
+        return dx
     _lib.check(_L().gvl_layernorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
                                       w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                                       dx.stride(0), int(accumulate_dx), _p(dw), _p(db),

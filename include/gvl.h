@@ -117,6 +117,14 @@ int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx,
                       void* dx, int64_t lddx, int32_t accumulate_dx,
                       void* dw, void* db, int32_t accumulate_wb, void* workspace,
                       int64_t rows, int64_t cols, gvl_stream_t stream);
+/* dx = res + LayerNorm backward (the residual-stream gradient of a pre-LN block:
+ * source/gpt2/train_gpt2.py:72-73, x + attn(ln_1(x)) / x + mlp(ln_2(x))) with the residual
+ * read from its own buffer, so the caller needs no copy of it; otherwise as above. */
+int gvl_layernorm_bwd_res(const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                          const void* w, const float* mean, const float* rstd,
+                          const void* res, int64_t ldr, void* dx, int64_t lddx,
+                          void* dw, void* db, int32_t accumulate_wb, void* workspace,
+                          int64_t rows, int64_t cols, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* Fused attention, head dim 64, bf16 in/out, fp32 online softmax.

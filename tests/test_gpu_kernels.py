@@ -525,6 +525,34 @@ def test_gemm_dropout_gate(cuda):
     assert 0.08 < frac < 0.12
 
 
+@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, "gemm_w4_kernel"),
+                                         (4096, 3072, 768, "gemm_pp3_kernel"),
+                                         (200, 136, 72, None), (4096, 768, 3072, None)])
+def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
+    """Compile-time bias + dropout + residual epilogue (EPI_BIAS_DROP_RES, the Q-Former's
+    out_proj / MLP output branches) in the four-wave and persistent kernels, and the same op
+    on the generic paths: mask = the counter hash of (m, n), exactly as the numpy restatement."""
+    K_ = _k()
+    torch.manual_seed(M + N + Kd)
+    x = torch.randn(M, Kd).to(BF)
+    w = (torch.randn(N, Kd) * 0.05).to(BF)
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    p, seed = 0.1, 123456789
+    A, B = x.to(cuda), w.to(cuda)
+    if kern is not None:
+        name = _kernel_name(A, B, 0, 0, M, N, Kd)
+        assert name.startswith(kern), name
+    y = K_.gemm(A, B, bias=bias.to(cuda), residual=res.to(cuda), drop_p=p, seed=seed)
+    h = x.float() @ w.float().t() + bias.float()
+    keep = torch.from_numpy(keep_mask(seed, np.arange(M * N), p).reshape(M, N))
+    ref = res.float() + torch.where(keep, h / (1 - p), torch.zeros_like(h))
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+    # every dropped element is exactly the residual
+    yd = y.float().cpu()[~keep]
+    assert torch.equal(yd, res.float()[~keep])
+
+
 # ------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("rows,C", [(37, 128), (300, 768), (5, 1024), (20011, 768), (1000, 520)])
 def test_layernorm_fwd_bwd(cuda, rows, C):
@@ -556,6 +584,13 @@ def test_layernorm_fwd_bwd(cuda, rows, C):
                      accumulate_wb=True)
     assert rel_err(dw.float().cpu().numpy(), (dw0 + wr.grad).numpy()) < 1e-2
     assert rel_err(db.float().cpu().numpy(), (db0 + br.grad).numpy()) < 1e-2
+    # residual read from its own buffer (gvl_layernorm_bwd_res): dx = prev + LN backward,
+    # prev untouched
+    prev_d = prev.to(cuda)
+    dx2 = torch.full((rows, C), float("nan"), dtype=BF, device=cuda)
+    K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd, dx=dx2, residual=prev_d)
+    assert rel_err(dx2.float().cpu().numpy(), (xr.grad + prev.float()).numpy()) < 1e-2
+    assert torch.equal(prev_d.cpu(), prev)
 
 
 # ------------------------------------------------------------------------- attention
