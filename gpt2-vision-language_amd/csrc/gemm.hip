@@ -203,12 +203,13 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.ws_bytes = p.ws ? d->workspace_bytes : 0;
   p.tickets = d->tickets;
   p.nticket = d->tickets ? d->ticket_count : 0;
+  p.batch = 1;
 }
 
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 10, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 11, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -226,9 +227,10 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
     } else if ((env().cfg < 0 || env().cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, env().cfg == 10)) {
+      // (cfg 11: default routing with the four-wave kernel off)
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       snprintf(buf, len, "gemm_w4_kernel<3, %s, %s>", tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
-    } else if (env().cfg >= 0) {
+    } else if (env().cfg >= 0 && env().cfg != 11) {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg == 10 ? 3 : env().cfg),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);
     } else if (gvl::gemm_pp3_plan(p, false)) {
@@ -279,9 +281,9 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     if (env().cfg == 10 && gvl::gemm_w4_plan(p, d->a_mn, true)) {
       gvl::gemm_w4_launch(p, d->b_mn, s);
-    } else if (env().cfg >= 0) {
+    } else if (env().cfg >= 0 && env().cfg != 11) {
       gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg == 10 ? 3 : env().cfg, s);
-    } else if (gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
+    } else if (env().cfg != 11 && gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
     } else if (env().impl == 4 && gvl::gemm_8p_try(p, d->a_mn, d->b_mn, false, s)) {
     } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
       gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn), s);
@@ -309,5 +311,67 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   else if (d->a_mn && !d->b_mn) gvl::launch_timed(gemm_bf16_kernel<true, false>, dim3(grid), dim3(NT), 0, s, p);
   else gvl::launch_timed(gemm_bf16_kernel<true, true>, dim3(grid), dim3(NT), 0, s, p);
   GVL_LAUNCH_CHECK("gvl_gemm");
+  return 0;
+}
+
+// Batched GEMM: count problems of one shape / layout (only the operand pointers differ), as
+// one persistent launch of gemm_pp3_kernel whose work items walk every problem's tiles — the
+// deferred weight gradients of the 12 GPT-2 blocks (gvl/functional.py): each is too small
+// (9-36 tiles of 256x256 at K = 16384 tokens) to fill the chip without a K split and fp32
+// slabs, together they do.  Epilogue: plain or C += AB (residual == c, fused accumulation);
+// anything else, or an unsupported shape, runs the problems one by one through gvl_gemm.
+extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream) {
+  GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_batched: bad arguments");
+  bool ok = count > 1 && count <= GVL_MAX_BATCH && env().impl >= 3 && env().cfg < 0;
+  for (int i = 0; ok && i < count; ++i) {
+    const gvl_gemm_desc& e = d[i];
+    ok = gvl::gemm_ring_ok(&e) && e.m == d[0].m && e.n == d[0].n && e.k == d[0].k &&
+         e.lda == d[0].lda && e.ldb == d[0].ldb && e.ldc == d[0].ldc && e.a_mn == d[0].a_mn &&
+         e.b_mn == d[0].b_mn && e.alpha == d[0].alpha && !e.alpha_ptr && !e.bias && !e.act &&
+         !e.dact && !e.gate && e.drop_p == 0.f && !e.c_fp32 && e.m > 0 && e.n > 0 &&
+         gvl::aligned16(e.c) && (e.residual == nullptr || (e.residual == e.c && e.ldr == e.ldc)) &&
+         ((e.residual == nullptr) == (d[0].residual == nullptr));
+  }
+  if (!ok) {
+    for (int i = 0; i < count; ++i) {
+      const int rc = gvl_gemm(&d[i], stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  GemmP p;
+  fill_params(&d[0], p);
+  p.ws = nullptr;  // whole-K tiles: the batch fills the chip
+  p.ws_bytes = 0;
+  p.tickets = nullptr;
+  p.nticket = 0;
+  p.batch = count;
+  for (int i = 0; i < count; ++i) {
+    p.Ab[i] = static_cast<const bf16_t*>(d[i].a);
+    p.Bb[i] = static_cast<const bf16_t*>(d[i].b);
+    p.Cb[i] = d[i].c;
+  }
+  if (gvl::gemm_pp3_plan(p, true) && p.splits == 1) {
+    // tile shape for the whole batch (the plan sized it for one problem): 256 rows, 256 or
+    // 192 columns, whichever fills the last round of CUs better (192 counted at 0.9)
+    const int64_t cus = gvl::num_cus(), tm = (p.M + 255) / 256;
+    auto fill = [&](int64_t tiles) {
+      return (double)tiles / (double)(((tiles + cus - 1) / cus) * cus);
+    };
+    const double e256 = fill(count * tm * ((p.N + 255) / 256));
+    const double e192 = (p.N % 64 == 0 && p.N >= 384) ? 0.9 * fill(count * tm * ((p.N + 191) / 192)) : 0.0;
+    p.bm = 256;
+    p.bn = e192 > e256 ? 192 : 256;
+    p.tiles_m = (int)tm;
+    p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
+  } else {
+    for (int i = 0; i < count; ++i) {
+      const int rc = gvl_gemm(&d[i], stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  gvl::gemm_pp3_launch(p, d[0].a_mn, d[0].b_mn, gvl::as_stream(stream));
+  GVL_LAUNCH_CHECK("gvl_gemm_batched");
   return 0;
 }

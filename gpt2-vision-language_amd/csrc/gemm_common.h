@@ -3,6 +3,8 @@
 #include "common.h"
 #include "../../include/gvl.h"
 
+#define GVL_MAX_BATCH 16
+
 struct GemmP {
   const bf16_t* A;
   const bf16_t* B;
@@ -36,6 +38,12 @@ struct GemmP {
   // zero between calls; null -> partials go to gemm_splitk_reduce
   uint32_t* tickets;
   int64_t nticket;
+  // batched launch (gvl_gemm_batched, gemm_pp3_kernel): `batch` problems of one shape, work
+  // items batch-major, per-problem operands below (batch == 1: A, B, C, residual above)
+  int batch;
+  const bf16_t* Ab[GVL_MAX_BATCH];
+  const bf16_t* Bb[GVL_MAX_BATCH];
+  void* Cb[GVL_MAX_BATCH];
 };
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
@@ -214,9 +222,10 @@ struct EpiPre {
     }
   }
   // rows of fragments i0 .. i0 + XH - 1
-  GVL_DEV void load_aux(const GemmP& p, int64_t mw0, int64_t nw0, int lane, int i0) {
+  GVL_DEV void load_aux(const GemmP& p, int64_t mw0, int64_t nw0, int lane, int i0,
+                        const bf16_t* res = nullptr) {
     if constexpr (KD::AUX) {
-      const bf16_t* base = KD::DACT ? p.pre_in : p.residual;
+      const bf16_t* base = KD::DACT ? p.pre_in : (res ? res : p.residual);
       const int64_t ld = KD::DACT ? p.ldp : p.ldr;
 #pragma unroll
       for (int i = 0; i < XH; ++i) {
@@ -298,7 +307,10 @@ static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a,
 // Odd FN: the last fragment is stored unpaired (8-B stores).
 template <int FM, int FN, int EPI = EPI_GEN>
 GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
-                             int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI>& pre) {
+                             int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI>& pre,
+                             void* cout = nullptr, const bf16_t* res = nullptr) {
+  // cout / res: this problem's C and residual in a batched launch (default p.C / p.residual)
+  bf16_t* const cbase = reinterpret_cast<bf16_t*>(cout ? cout : p.C);
   float gatev = 1.f;
   if constexpr (EPI == EPI_GEN) gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
   const bool plain = EPI == EPI_PLAIN ||
@@ -309,7 +321,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
   for (int i = 0; i < FM; ++i) {
     const int64_t m = mw0 + i * 16 + (lane & 15);
     const bool mok = m < p.M;
-    if (EpiKind<EPI>::AUX && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i);
+    if (EpiKind<EPI>::AUX && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i, res);
 #pragma unroll
     for (int j = 0; j + 1 < FN; j += 2) {
       const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
@@ -346,8 +358,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
       const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
       const int64_t n = nw0 + 16 * (j + (q & 1)) + 8 * (q >> 1);
       if (mok && n < p.N)
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n) =
-            make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        *reinterpret_cast<uint4*>(cbase + m * p.ldc + n) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
     }
     if constexpr (FN % 2 == 1) {
       constexpr int j = FN - 1;
@@ -369,7 +380,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
               make_uint2(pack2(h0[0], h0[1]), pack2(h0[2], h0[3]));
       }
       if (mok && n0 < p.N)
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + n0) = make_uint2(x0, y0);
+        *reinterpret_cast<uint2*>(cbase + m * p.ldc + n0) = make_uint2(x0, y0);
     }
   }
 }
@@ -481,6 +492,7 @@ int gemm_pp3_launch_tt(const GemmP& p, hipStream_t s);
 int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
 bool gemm_8p_plan(GemmP& p, bool force);
 bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
+int gemm_pp3_launch_batched(GemmP& p, int a_mn, int b_mn, hipStream_t s);  // p.batch > 1
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);

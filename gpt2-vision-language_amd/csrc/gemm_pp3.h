@@ -54,17 +54,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = wave >> 2, wc = wave & 3;
 
-  const int total = p.tiles_m * p.tiles_n * p.splits;
+  const int per_batch = p.tiles_m * p.tiles_n * p.splits;
+  const int total = per_batch * p.batch;
   const int G = gridDim.x, b = blockIdx.x;
   const int ntl = (total - b + G - 1) / G;  // work items of this workgroup
   const int nks = (int)(p.kper / KS);
   const int nsteps = ntl * nks;
   // work item of local item t: XCD-contiguous remap over the virtual grid of `total` items
-  // (G % 8 == 0 keeps b + tG on workgroup b's XCD), then the L2-grouped walk
-  auto tile_coords = [&](int t, int64_t& m0, int64_t& n0, int64_t& k0, int& split) {
+  // (G % 8 == 0 keeps b + tG on workgroup b's XCD), then the batch (batch-major: a problem's
+  // tiles stay together on an XCD) and the L2-grouped walk inside it
+  auto tile_coords = [&](int t, int64_t& m0, int64_t& n0, int64_t& k0, int& split, int& bi) {
     const int vid = b + t * G;
     const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
-    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
+    int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
+    bi = work / per_batch;
+    work -= bi * per_batch;
     int tm, tn;
     gemm_tile_of(work, p.splits, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
     m0 = (int64_t)tm * BM;
@@ -73,16 +77,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   };
 
   const int64_t a_rows = AMN ? p.K : p.M, b_rows = BMN ? p.K : p.N;
-  const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
-  const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
+  __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
+  __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
   const int sa_step = SA::step_bytes(p.lda), sb_step = SB::step_bytes(p.ldb);
   // issue cursor (steps are issued strictly in order)
   int is_t = 0, is_k = 0;
   int offa[SA::PER], offb[SB::PER];
   {
     int64_t m0, n0, k0;
-    int sp;
-    tile_coords(0, m0, n0, k0, sp);
+    int sp, bi;
+    tile_coords(0, m0, n0, k0, sp, bi);
+    if (p.batch > 1) {
+      ra = uniform_rsrc(p.Ab[bi], a_rows * p.lda * 2);
+      rb = uniform_rsrc(p.Bb[bi], b_rows * p.ldb * 2);
+    }
     SA::base_offsets(p.lda, m0, k0, wave, lane, offa);
     SB::base_offsets(p.ldb, n0, k0, wave, lane, offb);
   }
@@ -97,8 +105,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
         is_k = 0;                                                                   \
         if (++is_t < ntl) {                                                         \
           int64_t m0_, n0_, k0_;                                                    \
-          int sp_;                                                                  \
-          tile_coords(is_t, m0_, n0_, k0_, sp_);                                    \
+          int sp_, bi_;                                                             \
+          tile_coords(is_t, m0_, n0_, k0_, sp_, bi_);                               \
+          if (p.batch > 1) {                                                        \
+            ra = uniform_rsrc(p.Ab[bi_], a_rows * p.lda * 2);                       \
+            rb = uniform_rsrc(p.Bb[bi_], b_rows * p.ldb * 2);                       \
+          }                                                                         \
           SA::base_offsets(p.lda, m0_, k0_, wave, lane, offa);                      \
           SB::base_offsets(p.ldb, n0_, k0_, wave, lane, offb);                      \
         }                                                                           \
@@ -129,8 +141,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   int cu_t = 0, cu_k = 0;  // compute cursor
   int64_t cu_m0, cu_n0, cu_k0;
-  int cu_sp;
-  tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp);
+  int cu_sp, cu_bi;
+  tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
   EpiPre<FM, FN, EPI> pre;
   pre.load_bias(p, cu_n0 + bcol, lane);
 #define GVL_PP3_EPILOGUE()                                                                   \
@@ -146,7 +158,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
       gemm_store_partial<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane);           \
       epi_ = false;                                                                          \
     }                                                                                        \
-    if (epi_) gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre); \
+    if (epi_) {                                                                              \
+      void* c_ = p.batch > 1 ? p.Cb[cu_bi] : p.C;                                           \
+      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_,   \
+                                   p.batch > 1 ? static_cast<const bf16_t*>(c_) : p.residual); \
+    }                                                                                        \
   } while (0)
 
   short8_t af[FM], bf[FN];
@@ -159,7 +175,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
       ++cu_t;
-      tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp);
+      tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
       pre.load_bias(p, cu_n0 + bcol, lane);
     }
     const char* sl = smem + (c % NS) * SLOT;
@@ -203,7 +219,7 @@ int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  const int total = p.tiles_m * p.tiles_n * p.splits;
+  const int total = p.tiles_m * p.tiles_n * p.splits * p.batch;
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
   gvl::launch_timed(kern, dim3(grid), dim3(512), lds, s, p);
   if (p.splits > 1 && !(p.splits == 2 && p.tickets)) gvl::gemm_splitk_reduce_launch(p, s);

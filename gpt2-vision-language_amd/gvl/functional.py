@@ -86,6 +86,46 @@ FUSE_GRAD_ACC = True
 # stores x and recomputes gelu'(x) in the dX epilogue (act 1/2, dact 1/2).
 GELU_DERIV = 0 if os.environ.get("GVL_GELU_DERIV", "1") == "0" else 2
 _READY_HOOKS = []
+# Deferred weight gradients: a sunk nn.Linear weight gradient (dY^T X added into .grad) is
+# queued instead of launched, and at the end of the backward pass (an autograd engine final
+# callback) the queue runs as one batched persistent GEMM per shape (gvl_gemm_batched): the
+# 12 GPT-2 blocks' c_attn / attn.c_proj / c_fc / mlp.c_proj weight gradients (K = the
+# micro-step's 16k tokens) are 9-36 output tiles each — alone they need a K split with fp32
+# slabs and a reduce kernel to fill the chip, batched they fill it with whole-K tiles.
+# GVL_DEFER_WGRAD=0 launches each one in place.
+DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
+_PENDING = []          # (param, grad sink, dy2, x2, stream)
+_FLUSH_QUEUED = [False]
+
+
+def flush_wgrads():
+    """Run the queued weight gradients (batched by shape), then notify the grad-ready hooks.
+    Runs by itself at the end of every backward pass that queued any; harmless when empty."""
+    _FLUSH_QUEUED[0] = False
+    if not _PENDING:
+        return
+    pend = list(_PENDING)
+    _PENDING.clear()
+    groups = {}
+    for p, g, dy2, x2, st in pend:
+        key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
+               dy2.device, st)
+        groups.setdefault(key, []).append((p, g, dy2, x2))
+    for key, items in groups.items():
+        with torch.cuda.stream(key[-1]):
+            for i in range(0, len(items), 16):
+                chunk = items[i:i + 16]
+                K.gemm_batched([(dy2, x2, g, True) for _, g, dy2, x2 in chunk], a_mn=True,
+                               b_mn=True)
+                for p, *_ in chunk:
+                    _ready(p)
+
+
+def _defer_wgrad(p, g, dy2, x2):
+    _PENDING.append((p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
+    if not _FLUSH_QUEUED[0]:
+        _FLUSH_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(flush_wgrads)
 
 
 def register_grad_ready_hook(fn):
@@ -139,6 +179,9 @@ def _wgrad(ctx, i, p, dy2, x2):
     g = _sink(p, ctx)
     if g is None:
         return K.linear_dw(dy2, x2)
+    if DEFER_WGRAD:  # dy2 and x2 must stay unmodified until the end of the backward pass
+        _defer_wgrad(p, g, dy2, x2)
+        return None
     K.linear_dw(dy2, x2, out=g, residual=g)
     _ready(p)
     return None
@@ -245,8 +288,9 @@ class GPTBlockFn(torch.autograd.Function):
         g[3] = _wgrad(ctx, 3, P[3], dqkv, xn1)
         g[4] = _bgrad(ctx, 4, P[4], dqkv)
         dxn1 = K.linear_dx(dqkv, attn_w)
-        g[1], g[2] = _ln_bwd(ctx, 1, 2, P[1], P[2], dxn1, x2, m1, r1, dxm, True)
-        g[0] = dxm.view(B, T, C) if _need(ctx, 0) else None
+        dx = torch.empty_like(dxm)  # dxm stays intact: the (deferred) c_proj dW reads it
+        g[1], g[2] = _ln_bwd(ctx, 1, 2, P[1], P[2], dxn1, x2, m1, r1, dx, True, residual=dxm)
+        g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
         return tuple(g)
 
 

@@ -212,6 +212,40 @@ def linear_dw(dy2, x2, **kw):
     return gemm(dy2, x2, a_mn=True, b_mn=True, **kw)
 
 
+def gemm_batched(items, *, a_mn=False, b_mn=False):
+    """items: [(a, b, out, accumulate)] of one shape and layout: out (+)= op(a) @ op(b) for
+    every item as ONE persistent launch (gvl_gemm_batched; falls back to one launch each
+    when the library cannot batch them)."""
+    n = len(items)
+    if n == 0:
+        return
+    arr = (GemmDesc * n)()
+    ws = None
+    for i, (a, b, out, acc) in enumerate(items):
+        _dev(a, b)
+        _rowmajor(a, "A")
+        _rowmajor(b, "B")
+        _rowmajor(out, "C")
+        if a.dtype != BF16 or b.dtype != BF16 or out.dtype != BF16:
+            raise TypeError("gvl.gemm_batched: operands must be bf16")
+        M, K_ = (a.shape[1], a.shape[0]) if a_mn else (a.shape[0], a.shape[1])
+        N, Kb = (b.shape[1], b.shape[0]) if b_mn else (b.shape[0], b.shape[1])
+        if K_ != Kb or tuple(out.shape) != (M, N):
+            raise ValueError("gvl.gemm_batched: shape mismatch")
+        d = arr[i]
+        d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+        d.m, d.n, d.k = M, N, K_
+        d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), out.stride(0)
+        d.a_mn, d.b_mn = int(a_mn), int(b_mn)
+        d.alpha = 1.0
+        if acc:
+            d.residual, d.ldr = out.data_ptr(), out.stride(0)
+        if ws is None:
+            ws = _gemm_workspace(a.device)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    _lib.check(_L().gvl_gemm_batched(arr, n, _stream()), "gvl_gemm_batched")
+
+
 # ------------------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x2, w, b, eps=1e-5, out=None, stats=True):
     _dev(x2)

@@ -90,12 +90,20 @@ typedef struct gvl_gemm_desc {
   int64_t ticket_count;
 } gvl_gemm_desc;
 int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
+/* count (<= 16) GEMMs of one shape and layout that differ only in a, b, c (and residual,
+ * which is null for all or equal to c for all: C += AB) as ONE persistent launch: the
+ * weight gradients of the 12 GPT-2 blocks of a micro-step (source/gpt2/train_gpt2.py:471,
+ * loss.backward() -> the nn.Linear weight grads of every Block), each of which alone is too
+ * few output tiles to fill the chip.  Other epilogues / shapes run one by one. */
+int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):
  * impl 3 (default) = persistent ping-pong 256x256 kernel (split-K for few tiles) where
  * the work items fill the chip, else the 128x128 LDS-DMA ring; 2 = ring / non-persistent
  * ping-pong family; 1 = LDS-DMA v2 (K % 64 == 0); 0 = register-staged kernel always.
  * cfg -1 = pick by shape; otherwise forces a tile config of the family (impl 2: 0 = 256x256,
- * 1 = 256x128, 2 = 128x128, 3 = 256x256/5 slots, 4/5 = ping-pong, 6 = 64x128). */
+ * 1 = 256x128, 2 = 128x128, 3 = 256x256/5 slots, 4/5 = ping-pong, 6 = 64x128); impl 3:
+ * cfg 10 forces the four-wave 192x128 kernel where it applies, 11 = default routing
+ * without it. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
  * caller attribute event timings to the rocprofv3 kernel-trace rows). */

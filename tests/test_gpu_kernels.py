@@ -243,7 +243,12 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
     b = (torch.randn(K, N) * 0.05).to(BF)
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
-    name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
+    from gvl import _lib
+    _lib.lib().gvl_gemm_tune(3, 11)  # default routing minus the four-wave kernel (gemm_w4)
+    try:
+        name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
     assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 256>"), name
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
@@ -269,6 +274,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
         kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
     outs = []
     K_.SPLIT_COMBINE = True
+    _lib.lib().gvl_gemm_tune(3, 11)
     try:
         for _ in range(2):
             if epi == "res_inplace":
@@ -277,6 +283,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
             outs.append(K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw))
     finally:
         K_.SPLIT_COMBINE = False
+        _lib.lib().gvl_gemm_tune(3, -1)
     torch.cuda.synchronize()
     assert rel_err(outs[0].float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     assert torch.equal(outs[0], outs[1])
@@ -551,6 +558,26 @@ def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
     # every dropped element is exactly the residual
     yd = y.float().cpu()[~keep]
     assert torch.equal(yd, res.float()[~keep])
+
+
+@pytest.mark.parametrize("count,M,N,K,acc", [(12, 768, 768, 4096, True), (12, 2304, 768, 2048, True),
+                                             (3, 3072, 768, 1024, False), (2, 200, 136, 96, True),
+                                             (17, 256, 256, 64, True)])
+def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
+    """gvl_gemm_batched: `count` weight-gradient GEMMs dW_i (+)= dY_i^T X_i (both operands
+    MN-contiguous, as the deferred GPT-2 block weight gradients) in one persistent launch;
+    each equals its own reference.  count 17 (> 16) and a ragged shape exercise the fallback."""
+    K_ = _k()
+    torch.manual_seed(count + M + N + K)
+    dys = [torch.randn(K, M).to(BF) for _ in range(count)]
+    xs = [(torch.randn(K, N) * 0.1).to(BF) for _ in range(count)]
+    c0 = [torch.randn(M, N).to(BF) for _ in range(count)]
+    outs = [c.to(cuda) for c in c0]
+    K_.gemm_batched([(dy.to(cuda), x.to(cuda), o, acc) for dy, x, o in zip(dys, xs, outs)],
+                    a_mn=True, b_mn=True)
+    for dy, x, c, o in zip(dys, xs, c0, outs):
+        ref = dy.float().t() @ x.float() + (c.float() if acc else 0)
+        assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
 # ------------------------------------------------------------------------- LayerNorm
