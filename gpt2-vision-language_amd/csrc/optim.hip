@@ -212,6 +212,13 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __res
   if (!half && cc < cols) ws[(int64_t)blockIdx.y * cols + cc] = t + red[0][i];
 }
 
+// Batched column sums (gvl_colsum_batched): problem blockIdx.z (partial) / blockIdx.y (finish)
+constexpr int CS_MAX_BATCH = 16;
+struct ColsumBatch {
+  const bf16_t* x[CS_MAX_BATCH];
+  bf16_t* out[CS_MAX_BATCH];
+};
+
 // Block: 32 columns x 8 partial groups; each thread sums <= 16 partials (independent loads).
 __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restrict__ ws, int nb,
                                                             int64_t cols, bf16_t* __restrict__ out,
@@ -226,6 +233,79 @@ __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restr
     for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) {
       const int k = g + 8 * j;
       v[j] = k < nb ? ws[(int64_t)k * cols + c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) s += v[j];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g != 0 || c >= cols) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t += red[k][cl];
+  if (acc) t += bf2f(out[c]);
+  out[c] = f2bf(t);
+}
+
+__global__ __launch_bounds__(256) void colsum_partial_batched_kernel(ColsumBatch bt, int64_t rows,
+                                                                     int64_t cols, int64_t ld,
+                                                                     int64_t chunk, float* ws) {
+  // one problem per blockIdx.z; the body is colsum_partial_kernel's
+  __shared__ float red[16][CS_COLS + 4];
+  const bf16_t* __restrict__ x = bt.x[blockIdx.z];
+  float* __restrict__ w = ws + (int64_t)blockIdx.z * gridDim.y * cols;
+  const int ct = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int64_t c = (int64_t)blockIdx.x * CS_COLS + ct * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + rg;
+    for (; r + 112 < r1; r += 128) {
+      uint4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const uint4*>(x + (r + 16 * k) * ld + c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[0] += lo_bf(u[k].x); s[1] += hi_bf(u[k].x); s[2] += lo_bf(u[k].y); s[3] += hi_bf(u[k].y);
+        s[4] += lo_bf(u[k].z); s[5] += hi_bf(u[k].z); s[6] += lo_bf(u[k].w); s[7] += hi_bf(u[k].w);
+      }
+    }
+    for (; r < r1; r += 16) {
+      const uint4 u = *reinterpret_cast<const uint4*>(x + r * ld + c);
+      s[0] += lo_bf(u.x); s[1] += hi_bf(u.x); s[2] += lo_bf(u.y); s[3] += hi_bf(u.y);
+      s[4] += lo_bf(u.z); s[5] += hi_bf(u.z); s[6] += lo_bf(u.w); s[7] += hi_bf(u.w);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][ct * 8 + k] = s[k];
+  __syncthreads();
+  const int i = threadIdx.x & (CS_COLS - 1), half = threadIdx.x >> 7;
+  const int64_t cc = (int64_t)blockIdx.x * CS_COLS + i;
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t += red[8 * half + g][i];
+  __syncthreads();
+  if (half) red[0][i] = t;
+  __syncthreads();
+  if (!half && cc < cols) w[(int64_t)blockIdx.y * cols + cc] = t + red[0][i];
+}
+
+__global__ __launch_bounds__(256) void colsum_finish_batched_kernel(const float* ws, int nb,
+                                                                    int64_t cols, ColsumBatch bt,
+                                                                    int acc) {
+  __shared__ float red[8][33];
+  const float* __restrict__ w = ws + (int64_t)blockIdx.y * nb * cols;
+  bf16_t* __restrict__ out = bt.out[blockIdx.y];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t c = (int64_t)blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (c < cols) {
+    float v[CS_MAX_SPLITS / 8];
+#pragma unroll
+    for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) {
+      const int k = g + 8 * j;
+      v[j] = k < nb ? w[(int64_t)k * cols + c] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < CS_MAX_SPLITS / 8; ++j) s += v[j];
@@ -419,6 +499,51 @@ extern "C" int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld,
                      static_cast<const float*>(workspace), rows == 0 ? 1 : nb, cols,
                      static_cast<bf16_t*>(out), (int)accumulate);
   GVL_LAUNCH_CHECK("gvl_colsum(finish)");
+  return 0;
+}
+
+// Row splits per problem of a batched column sum: the whole launch still has >= ~768 blocks.
+static int colsum_blocks_batched(int64_t rows, int64_t cols, int count, int64_t* chunk) {
+  const int64_t cb = (cols + CS_COLS - 1) / CS_COLS;
+  int64_t nb = (768 + cb * count - 1) / (cb * count);
+  const int64_t by_rows = (rows + 63) / 64;
+  if (nb > by_rows) nb = by_rows;
+  if (nb > CS_MAX_SPLITS) nb = CS_MAX_SPLITS;
+  if (nb < 1) nb = 1;
+  *chunk = (rows + nb - 1) / nb;
+  return (int)nb;
+}
+
+extern "C" int64_t gvl_colsum_batched_workspace_size(int32_t count, int64_t rows, int64_t cols) {
+  int64_t chunk;
+  return (int64_t)count * colsum_blocks_batched(rows, cols, count, &chunk) * cols *
+         (int64_t)sizeof(float);
+}
+
+extern "C" int gvl_colsum_batched(const void* const* x, void* const* out, int32_t count,
+                                  int64_t rows, int64_t cols, int64_t ld, int32_t accumulate,
+                                  void* workspace, gvl_stream_t stream) {
+  GVL_REQUIRE(x && out && count >= 1 && count <= CS_MAX_BATCH,
+              "gvl_colsum_batched: 1..%d problems", CS_MAX_BATCH);
+  GVL_REQUIRE(cols % 8 == 0 && ld % 8 == 0 && rows > 0, "gvl_colsum_batched: bad shape");
+  GVL_REQUIRE(workspace, "gvl_colsum_batched: null workspace");
+  ColsumBatch bt{};
+  for (int i = 0; i < count; ++i) {
+    GVL_REQUIRE(x[i] && out[i] && gvl::aligned16(x[i]), "gvl_colsum_batched: bad operand %d", i);
+    bt.x[i] = static_cast<const bf16_t*>(x[i]);
+    bt.out[i] = static_cast<bf16_t*>(out[i]);
+  }
+  int64_t chunk;
+  const int nb = colsum_blocks_batched(rows, cols, count, &chunk);
+  hipStream_t s = gvl::as_stream(stream);
+  hipLaunchKernelGGL(colsum_partial_batched_kernel,
+                     dim3((unsigned)((cols + CS_COLS - 1) / CS_COLS), nb, count), dim3(256), 0, s,
+                     bt, rows, cols, ld, chunk, static_cast<float*>(workspace));
+  GVL_LAUNCH_CHECK("gvl_colsum_batched(partial)");
+  hipLaunchKernelGGL(colsum_finish_batched_kernel, dim3((unsigned)((cols + 31) / 32), count),
+                     dim3(256), 0, s, static_cast<const float*>(workspace), nb, cols, bt,
+                     (int)accumulate);
+  GVL_LAUNCH_CHECK("gvl_colsum_batched(finish)");
   return 0;
 }
 

@@ -106,6 +106,9 @@ SIGNATURES = {
                              c_vp]),
     "gvl_colsum_workspace_size": (c_i64, [c_i64, c_i64]),
     "gvl_colsum": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "gvl_colsum_batched_workspace_size": (c_i64, [c_i32, c_i64, c_i64]),
+    "gvl_colsum_batched": (C.c_int, [C.POINTER(c_vp), C.POINTER(c_vp), c_i32, c_i64, c_i64, c_i64,
+                                     c_i32, c_vp, c_vp]),
     "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,
                                          c_vp]),
     "gvl_gate_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -86,15 +86,19 @@ FUSE_GRAD_ACC = True
 # stores x and recomputes gelu'(x) in the dX epilogue (act 1/2, dact 1/2).
 GELU_DERIV = 0 if os.environ.get("GVL_GELU_DERIV", "1") == "0" else 2
 _READY_HOOKS = []
-# Deferred weight gradients: a sunk nn.Linear weight gradient (dY^T X added into .grad) is
-# queued instead of launched, and at the end of the backward pass (an autograd engine final
+# Deferred weight gradients: a sunk nn.Linear weight gradient (dY^T X added into .grad) and
+# bias gradient (column sums of dY) are queued instead of launched, and at the end of the backward pass (an autograd engine final
 # callback) the queue runs as one batched persistent GEMM per shape (gvl_gemm_batched): the
 # 12 GPT-2 blocks' c_attn / attn.c_proj / c_fc / mlp.c_proj weight gradients (K = the
 # micro-step's 16k tokens) are 9-36 output tiles each — alone they need a K split with fp32
-# slabs and a reduce kernel to fill the chip, batched they fill it with whole-K tiles.
+# slabs and a reduce kernel to fill the chip, batched they fill it with whole-K tiles; the 48
+# bias column sums (96 small launches) become 4 launch pairs (gvl_colsum_batched).
+# Only the per-block units repeated 12 times defer (GPTBlockFn, CrossAttnFn); the two-layer
+# Q-Former / linear bridge launch theirs in place (measured: deferring them is 0.5 % slower).
 # GVL_DEFER_WGRAD=0 launches each one in place.
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
 _PENDING = []          # (param, grad sink, dy2, x2, stream)
+_PENDING_B = []        # (param, grad sink, dy2, stream): bias gradients = column sums of dy2
 _FLUSH_QUEUED = [False]
 
 
@@ -102,6 +106,20 @@ def flush_wgrads():
     """Run the queued weight gradients (batched by shape), then notify the grad-ready hooks.
     Runs by itself at the end of every backward pass that queued any; harmless when empty."""
     _FLUSH_QUEUED[0] = False
+    if _PENDING_B:
+        pb = list(_PENDING_B)
+        _PENDING_B.clear()
+        bgroups = {}
+        for p, g, dy2, st in pb:
+            bgroups.setdefault((tuple(dy2.shape), dy2.stride(0), dy2.device, st), []).append((p, g, dy2))
+        for key, items in bgroups.items():
+            with torch.cuda.stream(key[-1]):
+                for i in range(0, len(items), 16):
+                    chunk = items[i:i + 16]
+                    K.colsum_batched([d for _, _, d in chunk], [g for _, g, _ in chunk],
+                                     accumulate=True)
+                    for p, *_ in chunk:
+                        _ready(p)
     if not _PENDING:
         return
     pend = list(_PENDING)
@@ -122,7 +140,10 @@ def flush_wgrads():
 
 
 def _defer_wgrad(p, g, dy2, x2):
-    _PENDING.append((p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
+    if x2 is None:  # bias gradient
+        _PENDING_B.append((p, g, dy2, torch.cuda.current_stream(dy2.device)))
+    else:
+        _PENDING.append((p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
     if not _FLUSH_QUEUED[0]:
         _FLUSH_QUEUED[0] = True
         torch.autograd.Variable._execution_engine.queue_callback(flush_wgrads)
@@ -172,14 +193,14 @@ def _ready(p):
         fn(p)
 
 
-def _wgrad(ctx, i, p, dy2, x2):
+def _wgrad(ctx, i, p, dy2, x2, defer=False):
     """nn.Linear weight gradient dy2^T x2 of input i (accumulated in place when p sinks)."""
     if not _need(ctx, i):
         return None
     g = _sink(p, ctx)
     if g is None:
         return K.linear_dw(dy2, x2)
-    if DEFER_WGRAD:  # dy2 and x2 must stay unmodified until the end of the backward pass
+    if defer and DEFER_WGRAD:  # dy2 and x2 must stay unmodified until the end of backward
         _defer_wgrad(p, g, dy2, x2)
         return None
     K.linear_dw(dy2, x2, out=g, residual=g)
@@ -187,13 +208,16 @@ def _wgrad(ctx, i, p, dy2, x2):
     return None
 
 
-def _bgrad(ctx, i, p, dy2):
+def _bgrad(ctx, i, p, dy2, defer=False):
     """Bias gradient (column sum of dy2) of input i."""
     if not _need(ctx, i):
         return None
     g = _sink(p, ctx)
     if g is None:
         return K.colsum(dy2)
+    if defer and DEFER_WGRAD and dy2.shape[0] > 0 and dy2.stride(1) == 1:
+        _defer_wgrad(p, g.view(-1), dy2, None)
+        return None
     K.colsum(dy2, out=g, accumulate=True)
     _ready(p)
     return None
@@ -268,25 +292,25 @@ class GPTBlockFn(torch.autograd.Function):
         d2 = d2.contiguous()
         P = ctx.params
         # MLP c_proj
-        g[11] = _wgrad(ctx, 11, P[11], d2, h)
-        g[12] = _bgrad(ctx, 12, P[12], d2)
+        g[11] = _wgrad(ctx, 11, P[11], d2, h, defer=True)
+        g[12] = _bgrad(ctx, 12, P[12], d2, defer=True)
         dpre = K.linear_dx(d2, mproj_w, dact=3 if GELU_DERIV else 1, pre_in=hpre)
-        g[9] = _wgrad(ctx, 9, P[9], dpre, xn2)
-        g[10] = _bgrad(ctx, 10, P[10], dpre)
+        g[9] = _wgrad(ctx, 9, P[9], dpre, xn2, defer=True)
+        g[10] = _bgrad(ctx, 10, P[10], dpre, defer=True)
         dxn2 = K.linear_dx(dpre, fc_w)
         dxm = torch.empty_like(d2)  # = d2 + LN_2 backward (the residual read from d2, no copy)
         g[7], g[8] = _ln_bwd(ctx, 7, 8, P[7], P[8], dxn2, xm, m2, r2, dxm, True, residual=d2)
         # attention c_proj
-        g[5] = _wgrad(ctx, 5, P[5], dxm, y.view(B * T, C))
-        g[6] = _bgrad(ctx, 6, P[6], dxm)
+        g[5] = _wgrad(ctx, 5, P[5], dxm, y.view(B * T, C), defer=True)
+        g[6] = _bgrad(ctx, 6, P[6], dxm, defer=True)
         dy = K.linear_dx(dxm, aproj_w)
         dqkv = torch.empty(B * T, 3 * C, dtype=BF16, device=d2.device)
         q3 = qkv.view(B, T, 3 * C)
         dq3 = dqkv.view(B, T, 3 * C)
         K.attn_bwd(dy.view(B, T, C), q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], y, lse, H,
                    causal, dq3[:, :, :C], dq3[:, :, C:2 * C], dq3[:, :, 2 * C:])
-        g[3] = _wgrad(ctx, 3, P[3], dqkv, xn1)
-        g[4] = _bgrad(ctx, 4, P[4], dqkv)
+        g[3] = _wgrad(ctx, 3, P[3], dqkv, xn1, defer=True)
+        g[4] = _bgrad(ctx, 4, P[4], dqkv, defer=True)
         dxn1 = K.linear_dx(dqkv, attn_w)
         dx = torch.empty_like(dxm)  # dxm stays intact: the (deferred) c_proj dW reads it
         g[1], g[2] = _ln_bwd(ctx, 1, 2, P[1], P[2], dxn1, x2, m1, r1, dx, True, residual=dxm)
@@ -562,8 +586,8 @@ class CrossAttnFn(torch.autograd.Function):
         if _need(ctx, 10):
             g[10] = gacc.to(gate.dtype).view_as(gate)
         P = ctx.params
-        g[8] = _wgrad(ctx, 8, P[8], dbr, o.view(B * T, C))
-        g[9] = _bgrad(ctx, 9, P[9], dbr)
+        g[8] = _wgrad(ctx, 8, P[8], dbr, o.view(B * T, C), defer=True)
+        g[9] = _bgrad(ctx, 9, P[9], dbr, defer=True)
         do = K.linear_dx(dbr, c_w).view(B, T, C)
         dqp = torch.empty(B * T, C, dtype=BF16, device=d2.device)
         dkvp = torch.empty(B * S, 2 * C, dtype=BF16, device=d2.device)
@@ -571,10 +595,10 @@ class CrossAttnFn(torch.autograd.Function):
         dk3 = dkvp.view(B, S, 2 * C)
         K.attn_bwd(do, qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], o, lse, H, False,
                    dqp.view(B, T, C), dk3[:, :, :C], dk3[:, :, C:])
-        g[4] = _wgrad(ctx, 4, P[4], dqp, xn)
-        g[5] = _bgrad(ctx, 5, P[5], dqp)
-        g[6] = _wgrad(ctx, 6, P[6], dkvp, z2)
-        g[7] = _bgrad(ctx, 7, P[7], dkvp)
+        g[4] = _wgrad(ctx, 4, P[4], dqp, xn, defer=True)
+        g[5] = _bgrad(ctx, 5, P[5], dqp, defer=True)
+        g[6] = _wgrad(ctx, 6, P[6], dkvp, z2, defer=True)
+        g[7] = _bgrad(ctx, 7, P[7], dkvp, defer=True)
         if _need(ctx, 1):
             g[1] = K.linear_dx(dkvp, kv_w).view(B, S, C)
         dxn = K.linear_dx(dqp, q_w)

@@ -506,6 +506,24 @@ def colsum(x2, out=None, accumulate=False):
     return out
 
 
+def colsum_batched(xs, outs, accumulate=False):
+    """outs[i] (+)= column sums of xs[i] (one shape, <= 16 problems) in one launch pair."""
+    n = len(xs)
+    rows, cols = xs[0].shape
+    for x, o in zip(xs, outs):
+        _dev(x)
+        if tuple(x.shape) != (rows, cols) or x.stride(0) != xs[0].stride(0) or x.stride(1) != 1:
+            raise ValueError("gvl.colsum_batched: problems must share shape and row stride")
+        if o.dtype != BF16 or o.numel() != cols or not o.is_contiguous():
+            raise ValueError("gvl.colsum_batched: bad output")
+    ws = torch.empty(max(_L().gvl_colsum_batched_workspace_size(n, rows, cols), 4) // 4,
+                     dtype=F32, device=xs[0].device)
+    xa = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
+    oa = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+    _lib.check(_L().gvl_colsum_batched(xa, oa, n, rows, cols, xs[0].stride(0), int(accumulate),
+                                       ws.data_ptr(), _stream()), "gvl_colsum_batched")
+
+
 def dropout_mask_apply(x2, p, seed, out=None, seed_ptr=None):
     rows, cols = x2.shape
     if out is None:

@@ -281,6 +281,13 @@ int gvl_sample(const void* logits, int64_t ld, int32_t logits_fp32, int64_t rows
 int64_t gvl_colsum_workspace_size(int64_t rows, int64_t cols);
 int gvl_colsum(const void* x, int64_t rows, int64_t cols, int64_t ld, void* out,
                int32_t accumulate, void* workspace, gvl_stream_t stream);
+/* count (<= 16) column sums of one shape in one launch pair: out[i] (+)= colsum(x[i]) — the
+ * deferred bias gradients of the 12 GPT-2 blocks (train_gpt2.py:471, nn.Linear bias grads).
+ * workspace: gvl_colsum_batched_workspace_size(count, rows, cols) bytes. */
+int64_t gvl_colsum_batched_workspace_size(int32_t count, int64_t rows, int64_t cols);
+int gvl_colsum_batched(const void* const* x, void* const* out, int32_t count, int64_t rows,
+                       int64_t cols, int64_t ld, int32_t accumulate, void* workspace,
+                       gvl_stream_t stream);
 /* out[r][c] = in[r][c] * keep(seed, r*cols+c) / (1-p) — dropout backward, with the
  * same counter-based mask the GEMM epilogue applies. */
 int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_out,

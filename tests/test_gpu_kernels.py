@@ -580,6 +580,22 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
         assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
+@pytest.mark.parametrize("count,rows,cols", [(12, 16384, 2304), (12, 4096, 768), (3, 1000, 3080),
+                                             (1, 37, 8)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_colsum_batched(cuda, count, rows, cols, acc):
+    """gvl_colsum_batched (the deferred bias gradients): out_i (+)= column sums of x_i."""
+    K_ = _k()
+    torch.manual_seed(count + rows + cols)
+    xs = [torch.randn(rows, cols).to(BF) for _ in range(count)]
+    o0 = [torch.randn(cols).to(BF) for _ in range(count)]
+    outs = [o.to(cuda) for o in o0]
+    K_.colsum_batched([x.to(cuda) for x in xs], outs, accumulate=acc)
+    for x, o, r in zip(xs, o0, outs):
+        ref = x.float().sum(0) + (o.float() if acc else 0)
+        assert rel_err(r.float().cpu().numpy(), ref.numpy()) < 1e-2
+
+
 # ------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("rows,C", [(37, 128), (300, 768), (5, 1024), (20011, 768), (1000, 520)])
 def test_layernorm_fwd_bwd(cuda, rows, C):
