@@ -320,9 +320,12 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
 // (9-36 tiles of 256x256 at K = 16384 tokens) to fill the chip without a K split and fp32
 // slabs, together they do.  Epilogue: plain or C += AB (residual == c, fused accumulation);
 // anything else, or an unsupported shape, runs the problems one by one through gvl_gemm.
-extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream) {
+static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
+                             gvl_stream_t stream) {
   GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_batched: bad arguments");
   bool ok = count > 1 && count <= GVL_MAX_BATCH && env().impl >= 3 && env().cfg < 0;
+  // fused bias gradients: weight-gradient layout (both operands MN-contiguous), C += AB
+  if (dbias) ok = ok && d[0].a_mn && d[0].b_mn && d[0].residual != nullptr;
   for (int i = 0; ok && i < count; ++i) {
     const gvl_gemm_desc& e = d[i];
     ok = gvl::gemm_ring_ok(&e) && e.m == d[0].m && e.n == d[0].n && e.k == d[0].k &&
@@ -333,6 +336,7 @@ extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_strea
          ((e.residual == nullptr) == (d[0].residual == nullptr));
   }
   if (!ok) {
+    GVL_REQUIRE(!dbias, "gvl_gemm_batched_dbias: shape not batchable (use gvl_colsum)");
     for (int i = 0; i < count; ++i) {
       const int rc = gvl_gemm(&d[i], stream);
       if (rc) return rc;
@@ -341,6 +345,7 @@ extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_strea
   }
   GemmP p;
   fill_params(&d[0], p);
+  for (int i = 0; i < GVL_MAX_BATCH; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
   p.ws = nullptr;  // whole-K tiles: the batch fills the chip
   p.ws_bytes = 0;
   p.tickets = nullptr;
@@ -365,6 +370,7 @@ extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_strea
     p.tiles_m = (int)tm;
     p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
   } else {
+    GVL_REQUIRE(!dbias, "gvl_gemm_batched_dbias: shape not batchable (use gvl_colsum)");
     for (int i = 0; i < count; ++i) {
       const int rc = gvl_gemm(&d[i], stream);
       if (rc) return rc;
@@ -374,4 +380,14 @@ extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_strea
   gvl::gemm_pp3_launch(p, d[0].a_mn, d[0].b_mn, gvl::as_stream(stream));
   GVL_LAUNCH_CHECK("gvl_gemm_batched");
   return 0;
+}
+
+extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream) {
+  return gemm_batched_impl(d, nullptr, count, stream);
+}
+
+extern "C" int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
+                                      gvl_stream_t stream) {
+  GVL_REQUIRE(dbias != nullptr, "gvl_gemm_batched_dbias: null dbias");
+  return gemm_batched_impl(d, dbias, count, stream);
 }

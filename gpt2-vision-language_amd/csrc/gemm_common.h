@@ -44,6 +44,10 @@ struct GemmP {
   const bf16_t* Ab[GVL_MAX_BATCH];
   const bf16_t* Bb[GVL_MAX_BATCH];
   void* Cb[GVL_MAX_BATCH];
+  // optional per-problem bf16 [M] bias gradients, Db[i] += row sums of op(A_i) over K (the
+  // nn.Linear bias grad next to its weight grad dW = dY^T X: A = dY^T), computed by the
+  // weight-gradient tiles of the first column block with MFMAs against a ones fragment
+  void* Db[GVL_MAX_BATCH];
 };
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
@@ -492,7 +496,6 @@ int gemm_pp3_launch_tt(const GemmP& p, hipStream_t s);
 int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
 bool gemm_8p_plan(GemmP& p, bool force);
 bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
-int gemm_pp3_launch_batched(GemmP& p, int a_mn, int b_mn, hipStream_t s);  // p.batch > 1
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);

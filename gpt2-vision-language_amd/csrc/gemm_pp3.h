@@ -125,6 +125,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   const int arow = g * (BM / 2), bcol = wc * (BN / 4);
+  // fused bias gradient (batched weight-gradient launches, GemmP::Db): the tiles of column
+  // block 0 also sum their A fragments over K — MFMAs against a ones fragment, FM/4 of the
+  // wave group's FM row fragments per wave — and add the row sums into Db in the epilogue
+  constexpr bool DB = EPI == EPI_RES && AMN && BMN;
+  constexpr int FPW = FM / 4 > 0 ? FM / 4 : 1;
+  float4_t bacc[DB ? FPW : 1];
+#pragma unroll
+  for (int k = 0; k < (DB ? FPW : 1); ++k) bacc[k] = float4_t{0.f, 0.f, 0.f, 0.f};
+  short8_t ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
+  bool do_db = false;
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i) GVL_PP3_ISSUE(i);
   {
@@ -145,6 +157,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
   EpiPre<FM, FN, EPI> pre;
   pre.load_bias(p, cu_n0 + bcol, lane);
+  if constexpr (DB) do_db = p.batch > 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
 #define GVL_PP3_EPILOGUE()                                                                   \
   do {                                                                                       \
     bool epi_ = true;                                                                        \
@@ -163,6 +176,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
       gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_,   \
                                    p.batch > 1 ? static_cast<const bf16_t*>(c_) : p.residual); \
     }                                                                                        \
+    if constexpr (DB) {                                                                      \
+      if (do_db && (lane >> 4) == 0) {                                                       \
+        bf16_t* db_ = static_cast<bf16_t*>(p.Db[cu_bi]);                                     \
+        _Pragma("unroll") for (int k = 0; k < FPW; ++k) {                                    \
+          const int64_t m_ = cu_m0 + arow + 16 * (wc * FPW + k) + lane;                      \
+          if (m_ < p.M) db_[m_] = f2bf(bf2f(db_[m_]) + bacc[k][0] * alpha);                  \
+        }                                                                                    \
+      }                                                                                      \
+      _Pragma("unroll") for (int k = 0; k < FPW; ++k) bacc[k] = float4_t{0.f, 0.f, 0.f, 0.f}; \
+    }                                                                                        \
   } while (0)
 
   short8_t af[FM], bf[FN];
@@ -177,6 +200,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
       ++cu_t;
       tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
       pre.load_bias(p, cu_n0 + bcol, lane);
+      if constexpr (DB) do_db = p.batch > 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
     }
     const char* sl = smem + (c % NS) * SLOT;
 #pragma unroll
@@ -195,6 +219,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+    if constexpr (DB) {
+      if (do_db) {
+#pragma unroll
+        for (int k = 0; k < FPW; ++k) {  // wave-uniform branch: constant register indices
+          if (wc == 0) bacc[k] = mfma16(ones, af[k], bacc[k]);
+          else if (wc == 1) bacc[k] = mfma16(ones, af[(FPW + k) % FM], bacc[k]);
+          else if (wc == 2) bacc[k] = mfma16(ones, af[(2 * FPW + k) % FM], bacc[k]);
+          else bacc[k] = mfma16(ones, af[(3 * FPW + k) % FM], bacc[k]);
+        }
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     if (++cu_k == nks) cu_k = 0;
     {

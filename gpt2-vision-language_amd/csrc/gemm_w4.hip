@@ -117,6 +117,22 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
 #define W4_PRIO(x) __builtin_amdgcn_s_setprio(x)
 #endif
 
+// Timing-only diagnostic builds (wrong results; never the shipped library):
+// GVL_W4_DIAG=1 drops the per-step barrier, 2 drops the per-step LDS writes and global loads.
+#ifndef GVL_W4_DIAG
+#define GVL_W4_DIAG 0
+#endif
+#if GVL_W4_DIAG == 1
+#define W4_DIAG_BAR() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#else
+#define W4_DIAG_BAR() barrier_lds()
+#endif
+#if GVL_W4_DIAG == 2
+#define W4_DIAG_MEM(...) do {} while (0)
+#else
+#define W4_DIAG_MEM(...) do { __VA_ARGS__; } while (0)
+#endif
+
 template <int NS, bool BMN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
   constexpr int BM = W4_BM, BN = W4_BN, NW = 4, FM = 6, FN = 4, P = 3;
@@ -218,15 +234,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
           NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                           \
       _Pragma("unroll") for (int i = 0; i < FM; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
     }                                                                                       \
-    GVL_W4_WRITE((C) + 2, SET);                                                             \
-    GVL_W4_LOAD(SET);                                                                       \
+    W4_DIAG_MEM(GVL_W4_WRITE((C) + 2, SET); GVL_W4_LOAD(SET));                              \
     W4_PRIO(1);                                                                             \
     _Pragma("unroll") for (int i = 0; i < FM; ++i)                                          \
         _Pragma("unroll") for (int j = 0; j < FN; ++j)                                      \
             acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]);                                    \
     W4_PRIO(0);                                                                             \
     W4_INTERLEAVE();                                                                        \
-    barrier_lds();                                                                          \
+    W4_DIAG_BAR();                                                                          \
   } while (0)
 
   int c = 0;

@@ -71,6 +71,7 @@ SIGNATURES = {
     "gvl_set_launch_events": (C.c_int, [c_vp, c_vp]),
     "gvl_gemm": (C.c_int, [C.POINTER(GemmDesc), c_vp]),
     "gvl_gemm_batched": (C.c_int, [C.POINTER(GemmDesc), c_i32, c_vp]),
+    "gvl_gemm_batched_dbias": (C.c_int, [C.POINTER(GemmDesc), C.POINTER(c_vp), c_i32, c_vp]),
     "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
     "gvl_gemm_kernel_name": (C.c_int, [C.POINTER(GemmDesc), C.c_char_p, c_i32]),
     "gvl_layernorm_fwd": (C.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,

@@ -106,6 +106,48 @@ def flush_wgrads():
     """Run the queued weight gradients (batched by shape), then notify the grad-ready hooks.
     Runs by itself at the end of every backward pass that queued any; harmless when empty."""
     _FLUSH_QUEUED[0] = False
+    # a bias gradient over the same dY as a queued weight gradient rides in that batched GEMM
+    # (gvl_gemm_batched_dbias: row sums of dY^T from the same operand tiles)
+    paired = {}
+    if _PENDING_B and _PENDING:
+        wkeys = {(d.data_ptr(), tuple(d.shape), d.stride(0)) for _, _, d, _, _ in _PENDING}
+        rest = []
+        for p, g, dy2, st in _PENDING_B:
+            k = (dy2.data_ptr(), tuple(dy2.shape), dy2.stride(0))
+            if k in wkeys and k not in paired:
+                paired[k] = (p, g)
+            else:
+                rest.append((p, g, dy2, st))
+        _PENDING_B[:] = rest
+    if not _PENDING:
+        pend = []
+    else:
+        pend = list(_PENDING)
+        _PENDING.clear()
+    groups = {}
+    for p, g, dy2, x2, st in pend:
+        key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
+               dy2.device, st)
+        groups.setdefault(key, []).append((p, g, dy2, x2))
+    for key, items in groups.items():
+        with torch.cuda.stream(key[-1]):
+            for i in range(0, len(items), 16):
+                chunk = items[i:i + 16]
+                bias = [paired.get((d.data_ptr(), tuple(d.shape), d.stride(0))) for _, _, d, _ in chunk]
+                fused = all(b is not None for b in bias) and K.gemm_batched(
+                    [(dy2, x2, g, True) for _, g, dy2, x2 in chunk], a_mn=True, b_mn=True,
+                    dbias=[b[1] for b in bias])
+                if not fused:
+                    K.gemm_batched([(dy2, x2, g, True) for _, g, dy2, x2 in chunk], a_mn=True,
+                                   b_mn=True)
+                    for (_, _, d, _), b in zip(chunk, bias):
+                        if b is not None:
+                            _PENDING_B.append((b[0], b[1], d, key[-1]))
+                for p, *_ in chunk:
+                    _ready(p)
+                if fused:
+                    for b in bias:
+                        _ready(b[0])
     if _PENDING_B:
         pb = list(_PENDING_B)
         _PENDING_B.clear()
@@ -120,23 +162,6 @@ def flush_wgrads():
                                      accumulate=True)
                     for p, *_ in chunk:
                         _ready(p)
-    if not _PENDING:
-        return
-    pend = list(_PENDING)
-    _PENDING.clear()
-    groups = {}
-    for p, g, dy2, x2, st in pend:
-        key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
-               dy2.device, st)
-        groups.setdefault(key, []).append((p, g, dy2, x2))
-    for key, items in groups.items():
-        with torch.cuda.stream(key[-1]):
-            for i in range(0, len(items), 16):
-                chunk = items[i:i + 16]
-                K.gemm_batched([(dy2, x2, g, True) for _, g, dy2, x2 in chunk], a_mn=True,
-                               b_mn=True)
-                for p, *_ in chunk:
-                    _ready(p)
 
 
 def _defer_wgrad(p, g, dy2, x2):

@@ -212,10 +212,13 @@ def linear_dw(dy2, x2, **kw):
     return gemm(dy2, x2, a_mn=True, b_mn=True, **kw)
 
 
-def gemm_batched(items, *, a_mn=False, b_mn=False):
+def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
     """items: [(a, b, out, accumulate)] of one shape and layout: out (+)= op(a) @ op(b) for
     every item as ONE persistent launch (gvl_gemm_batched; falls back to one launch each
-    when the library cannot batch them)."""
+    when the library cannot batch them).  dbias (weight gradients only: a_mn = b_mn, every
+    item accumulating): bf16 [M] bias grads, dbias[i] += column sums of items[i]'s dY, fused
+    into the same launch (gvl_gemm_batched_dbias); returns False (nothing launched) when the
+    batch cannot run fused."""
     n = len(items)
     if n == 0:
         return
@@ -243,7 +246,14 @@ def gemm_batched(items, *, a_mn=False, b_mn=False):
         if ws is None:
             ws = _gemm_workspace(a.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    if dbias is not None:
+        for t in dbias:
+            if t.dtype != BF16 or not t.is_contiguous():
+                raise ValueError("gvl.gemm_batched: dbias must be contiguous bf16")
+        da = (C.c_void_p * n)(*[t.data_ptr() for t in dbias])
+        return _L().gvl_gemm_batched_dbias(arr, da, n, _stream()) == 0
     _lib.check(_L().gvl_gemm_batched(arr, n, _stream()), "gvl_gemm_batched")
+    return True
 
 
 # ------------------------------------------------------------------------- LayerNorm

@@ -96,6 +96,13 @@ int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream);
  * loss.backward() -> the nn.Linear weight grads of every Block), each of which alone is too
  * few output tiles to fill the chip.  Other epilogues / shapes run one by one. */
 int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream);
+/* As gvl_gemm_batched for weight gradients (a_mn = b_mn = 1, residual == c) that also add
+ * each problem's bias gradient: dbias[i] (bf16 [m]) += row sums of A_i^T over k, i.e. the
+ * column sums of dY — the nn.Linear bias grad beside its weight grad, computed from the same
+ * operand tiles (no second pass over dY).  Returns an error when the batch cannot run as one
+ * launch (the caller then uses gvl_gemm_batched + gvl_colsum_batched). */
+int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
+                           gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):
  * impl 3 (default) = persistent ping-pong 256x256 kernel (split-K for few tiles) where
  * the work items fill the chip, else the 128x128 LDS-DMA ring; 2 = ring / non-persistent

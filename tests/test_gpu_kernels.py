@@ -578,6 +578,18 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
     for dy, x, c, o in zip(dys, xs, c0, outs):
         ref = dy.float().t() @ x.float() + (c.float() if acc else 0)
         assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
+    if acc:  # fused bias gradients: db_i += column sums of dY_i, from the same launch
+        b0 = [torch.randn(M).to(BF) for _ in range(count)]
+        dbs = [b.to(cuda) for b in b0]
+        outs = [c.to(cuda) for c in c0]
+        fused = K_.gemm_batched([(dy.to(cuda), x.to(cuda), o, True) for dy, x, o in zip(dys, xs, outs)],
+                                a_mn=True, b_mn=True, dbias=dbs)
+        assert fused == (2 <= count <= 16)
+        if fused:
+            for dy, x, c, o, b, db in zip(dys, xs, c0, outs, b0, dbs):
+                ref = dy.float().t() @ x.float() + c.float()
+                assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
+                assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
 
 
 @pytest.mark.parametrize("count,rows,cols", [(12, 16384, 2304), (12, 4096, 768), (3, 1000, 3080),
