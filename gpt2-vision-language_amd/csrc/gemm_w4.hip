@@ -334,6 +334,9 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
   if (gemm_epi_kind(p) == EPI_GEN) return false;
   if (force || w4_mode() == 2) return true;
   if (w4_mode() == 0) return false;
+  // GVL_W4=3 (A/B): also the short-K wide outputs (K <= 1024, N <= 4096: c_attn / c_fc
+  // forward, mlp.c_proj dX), whose 192x256 ping-pong tiles run only 24 K-steps each.
+  if (w4_mode() == 3 && p.K <= 1024 && p.N <= 4096) return true;
   const int64_t cus = num_cus();
   const int64_t t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int64_t tw4 = ((p.M + W4_BM - 1) / W4_BM) * ((p.N + W4_BN - 1) / W4_BN);

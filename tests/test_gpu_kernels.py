@@ -342,7 +342,7 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
 @pytest.mark.parametrize("b_mn", [0, 1])
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "res_inplace", "bias_act_d", "mul", "dact_erf"])
 @pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 2304), (7992, 776, 192),
-                                   (16384, 768, 384), (300, 128, 192)])
+                                   (16384, 768, 384), (300, 128, 192), (8064, 3072, 768)])
 def test_gemm_w4(cuda, b_mn, epi, M, N, K):
     """Four-wave 192x128 deep-ring kernel (gemm_w4.hip), forced with gvl_gemm_tune(3, 10):
     the caption decoder's N = 768 shapes (252 tiles, one per CU), ragged M and N (N % 128 != 0),
