@@ -1,6 +1,6 @@
 """Time every GEMM shape of the LM and Q-Former steps: libgvl (default pick and forced
 configs) next to torch.mm (hipBLASLt) as a yardstick.  One process, HIP events.
-python tools/gemm_shapes.py [lm|qf|all] [impl:cfg comma list; 2:-1 = default pick]"""
+python tools/gemm_shapes.py [lm|qf|xa|all] [impl:cfg comma list; 2:-1 = default pick]"""
 import os
 import sys
 
@@ -13,6 +13,7 @@ from gvl import kernels as K  # noqa: E402
 T = 16384  # LM tokens per micro-step
 Q = 8064   # Q-Former caption rows (128 x 63)
 QT = 3968  # caption text rows (128 x 31)
+ZS = 4224  # cross-att vision rows (128 x 33)
 # (name, M, N, K, a_mn, b_mn)
 BIG = [("big8k", 8192, 8192, 8192, 0, 0)]
 LM = [
@@ -33,6 +34,17 @@ QF = [
     ("q.lm_head.dX", QT, 768, 50304, 0, 1),
     ("q.c_attn.dX", Q, 768, 2304, 0, 1), ("q.c_fc.dX", Q, 768, 3072, 0, 1),
     ("q.mlp.c_proj.dX", Q, 3072, 768, 0, 1), ("q.c_proj.dX", Q, 768, 768, 0, 1),
+]
+
+XA = [  # cross-att caption step: text-only decoder rows (QT) + 33 projected CLIP tokens (ZS)
+    ("x.q_proj", QT, 768, 768, 0, 0), ("x.kv_proj", ZS, 1536, 768, 0, 0),
+    ("x.c_attn", QT, 2304, 768, 0, 0), ("x.c_fc", QT, 3072, 768, 0, 0),
+    ("x.mlp.c_proj", QT, 768, 3072, 0, 0),
+    ("x.q_proj.dX", QT, 768, 768, 0, 1), ("x.kv_proj.dX", ZS, 768, 1536, 0, 1),
+    ("x.c_attn.dX", QT, 768, 2304, 0, 1), ("x.c_fc.dX", QT, 768, 3072, 0, 1),
+    ("x.mlp.c_proj.dX", QT, 3072, 768, 0, 1),
+    ("x.q_proj.dW", 768, 768, QT, 1, 1), ("x.kv_proj.dW", 1536, 768, ZS, 1, 1),
+    ("x.kv_all", ZS, 18432, 768, 0, 0), ("x.kv_all.dX", ZS, 768, 18432, 0, 1),  # CrossKVFn
 ]
 
 
@@ -77,7 +89,7 @@ def main():
         return epilogues()
     cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["2:-1"]
     shapes = ((BIG if which in ("big", "all") else []) + (LM if which in ("lm", "all") else [])
-              + (QF if which in ("qf", "all") else []))
+              + (QF if which in ("qf", "all") else []) + (XA if which in ("xa", "all") else []))
     L = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(0)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
