@@ -335,12 +335,19 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
   if (force || w4_mode() == 2) return true;
   if (w4_mode() == 0) return false;
   // GVL_W4=3 (A/B): also the short-K wide outputs (K <= 1024, N <= 4096: c_attn / c_fc
-  // forward, mlp.c_proj dX), whose 192x256 ping-pong tiles run only 24 K-steps each.
+  // forward, mlp.c_proj dX), whose 192x256 ping-pong tiles run only 24 K-steps each —
+  // measured slower (profiles/r2/r2i/w4s_shapes.txt: 575 vs 790 TF/s at M = 16384).
   if (w4_mode() == 3 && p.K <= 1024 && p.N <= 4096) return true;
   const int64_t cus = num_cus();
   const int64_t t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int64_t tw4 = ((p.M + W4_BM - 1) / W4_BM) * ((p.N + W4_BN - 1) / W4_BN);
-  return p.N <= 1024 && t256 < 160 && tw4 * 2 >= cus && tw4 <= cus;
+  if (p.N > 1024 || t256 >= 160 || tw4 > cus) return false;
+  if (w4_mode() == 4) return tw4 * 2 >= cus;  // GVL_W4=4: the round-2 half-chip rule (A/B)
+  if (tw4 * 4 >= cus * 3) return true;
+  // 40-75 % of the CUs (the cross-att decoder's 3968 text rows: 126 tiles) only with a K short
+  // enough that one tile per CU beats splitting K (the caption lm_head dX, K = 50304, and the
+  // cross-att batched kv_proj dX, K = 18432, do not)
+  return tw4 * 5 >= cus * 2 && p.K <= 4096;
 }
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {

@@ -6,6 +6,7 @@ frozen at (1, 0).  Compute: CrossAttnFn + GPTBlockFn per block on the HIP path.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -16,6 +17,10 @@ from .functional import bf
 from .gpt2 import MLP, build_optimizer, init_gpt_weights
 from .gpt2 import CausalSelfAttention as CausalSelfAttention  # with the mask buffer (:19)
 from .caption import pool_clip_197_to_33_avg_with_cls
+
+# kv_proj of all blocks as one GEMM over the shared z_proj (Fn.CrossKVFn); GVL_XKV_BATCH=0 runs
+# each block's own kv_proj inside Fn.CrossAttnFn (A/B).
+XKV_BATCH = os.environ.get("GVL_XKV_BATCH", "1") != "0"
 
 __all__ = ["GPTConfig", "CausalSelfAttention", "CrossAttention", "MLP", "Vision_projector",
            "Block", "GPT", "pool_clip_197_to_33_avg_with_cls"]
@@ -70,11 +75,18 @@ class Block(nn.Module):
         self.mlp = MLP(config)
         self.cross_gate = nn.Parameter(torch.tensor(0.0))
 
-    def forward(self, x, z):
+    def forward(self, x, z, kv=None):
+        """kv = (packed kv_proj of every block, this block's index, KVGradSlab) when the GPT
+        runs all kv_proj as one GEMM (Fn.CrossKVFn); None: this block's own kv_proj(z)."""
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
-        if z is not None:
-            xa = self.xattn
+        xa = self.xattn
+        if kv is not None:
+            x = Fn.CrossAttnKVFn.apply(x, kv[0], kv[1], kv[2], bf(self.ln_x.weight),
+                                       bf(self.ln_x.bias), bf(xa.q_proj.weight),
+                                       bf(xa.q_proj.bias), bf(xa.c_proj.weight),
+                                       bf(xa.c_proj.bias), bf(self.cross_gate), xa.n_head)
+        elif z is not None:
             x = Fn.CrossAttnFn.apply(x, z, bf(self.ln_x.weight), bf(self.ln_x.bias),
                                      bf(xa.q_proj.weight), bf(xa.q_proj.bias),
                                      bf(xa.kv_proj.weight), bf(xa.kv_proj.bias),
@@ -120,11 +132,15 @@ class GPT(nn.Module):
                                  f"{self.config.block_size}")
         tr = self.transformer
         x = Fn.EmbedFn.apply(idx, bf(tr.wte.weight), bf(tr.wpe.weight), None)
-        zp = None
+        zp = kv = None
         if z is not None:
             zp = tr.vis_proj(z).to(dtype=x.dtype)
-        for blk in tr.h:
-            x = blk(x, zp)
+            if XKV_BATCH and len(tr.h) > 1:
+                slab = Fn.KVGradSlab(len(tr.h))
+                wb = [bf(t) for blk in tr.h for t in (blk.xattn.kv_proj.weight, blk.xattn.kv_proj.bias)]
+                kv = Fn.CrossKVFn.apply(zp, slab, *wb)
+        for i, blk in enumerate(tr.h):
+            x = blk(x, zp, None if kv is None else (kv, i, slab))
         x = Fn.LayerNormFn.apply(x, bf(tr.ln_f.weight), bf(tr.ln_f.bias), 1e-5)
         w = bf(self.lm_head.weight)
         if targets is None:

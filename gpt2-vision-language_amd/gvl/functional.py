@@ -580,56 +580,160 @@ class CrossAttnFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, z, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b, gate, n_head: int):
-        B, T, C = x.shape
         S = z.shape[1]
-        x2 = x.reshape(B * T, C).contiguous()
-        z2 = z.reshape(B * S, C).to(BF16).contiguous()
-        xn, mean, rstd = K.layernorm_fwd(x2, ln_w, ln_b)
-        qp = K.linear(xn, q_w, q_b)
+        z2 = z.reshape(z.shape[0] * S, z.shape[2]).to(BF16).contiguous()
         kvp = K.linear(z2, kv_w, kv_b)
-        k3 = kvp.view(B, S, 2 * C)
-        o, lse = K.attn_fwd(qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], n_head, False)
-        ybr = torch.empty(B * T, C, dtype=BF16, device=x.device)
-        out = K.linear(o.view(B * T, C), c_w, c_b, residual=x2, gate=gate, pre_out=ybr)
-        if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
-            ctx.save_for_backward(x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w,
-                                  c_w, gate)
-            ctx.cfg = (B, T, S, C, n_head)
+        out = _xattn_fwd(ctx, x, kvp.view(z.shape[0], S, kvp.shape[1]), 0, ln_w, ln_b, q_w, q_b,
+                         c_w, c_b, gate, n_head)
+        if any(ctx.needs_input_grad):
+            ctx.z2, ctx.kv_w = z2, kv_w
             ctx.params = (None, None, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b)
-            _mark(ctx)
-        return out.view(B, T, C)
+            ctx.idx = (0, 2, 3, 4, 5, 8, 9, 10)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        (x2, z2, xn, mean, rstd, qp, kvp, o, lse, ybr, ln_w, q_w, kv_w, c_w,
-         gate) = ctx.saved_tensors
-        B, T, S, C, H = ctx.cfg
-        d2 = dout.reshape(B * T, C).to(BF16).contiguous()
         g = [None] * 12
-        gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
-        dbr = K.gate_bwd(d2, ybr, gate, gacc)
-        if _need(ctx, 10):
-            g[10] = gacc.to(gate.dtype).view_as(gate)
+        C = ctx.cfg[3]
+        dkvp = torch.empty(ctx.z2.shape[0], 2 * C, dtype=BF16, device=dout.device)
+        _xattn_bwd(ctx, dout, dkvp.view(ctx.cfg[0], ctx.cfg[2], 2 * C), g)
         P = ctx.params
-        g[8] = _wgrad(ctx, 8, P[8], dbr, o.view(B * T, C), defer=True)
-        g[9] = _bgrad(ctx, 9, P[9], dbr, defer=True)
-        do = K.linear_dx(dbr, c_w).view(B, T, C)
-        dqp = torch.empty(B * T, C, dtype=BF16, device=d2.device)
-        dkvp = torch.empty(B * S, 2 * C, dtype=BF16, device=d2.device)
-        k3 = kvp.view(B, S, 2 * C)
-        dk3 = dkvp.view(B, S, 2 * C)
-        K.attn_bwd(do, qp.view(B, T, C), k3[:, :, :C], k3[:, :, C:], o, lse, H, False,
-                   dqp.view(B, T, C), dk3[:, :, :C], dk3[:, :, C:])
-        g[4] = _wgrad(ctx, 4, P[4], dqp, xn, defer=True)
-        g[5] = _bgrad(ctx, 5, P[5], dqp, defer=True)
-        g[6] = _wgrad(ctx, 6, P[6], dkvp, z2, defer=True)
+        g[6] = _wgrad(ctx, 6, P[6], dkvp, ctx.z2, defer=True)
         g[7] = _bgrad(ctx, 7, P[7], dkvp, defer=True)
         if _need(ctx, 1):
-            g[1] = K.linear_dx(dkvp, kv_w).view(B, S, C)
-        dxn = K.linear_dx(dqp, q_w)
-        dx = torch.empty_like(d2)  # = d2 + LN backward (residual read from d2, no copy)
-        g[2], g[3] = _ln_bwd(ctx, 2, 3, P[2], P[3], dxn, x2, mean, rstd, dx, True, residual=d2)
-        g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
+            g[1] = K.linear_dx(dkvp, ctx.kv_w).view(ctx.cfg[0], ctx.cfg[2], C)
+        return tuple(g)
+
+
+def _xattn_fwd(ctx, x, kv, off, ln_w, ln_b, q_w, q_b, c_w, c_b, gate, n_head):
+    """Everything of the gated cross-attention but kv_proj: K = kv[..., off:off+C],
+    V = kv[..., off+C:off+2C] (strided views of the packed projection)."""
+    B, T, C = x.shape
+    S = kv.shape[1]
+    x2 = x.reshape(B * T, C).contiguous()
+    xn, mean, rstd = K.layernorm_fwd(x2, ln_w, ln_b)
+    qp = K.linear(xn, q_w, q_b)
+    o, lse = K.attn_fwd(qp.view(B, T, C), kv[:, :, off:off + C], kv[:, :, off + C:off + 2 * C],
+                        n_head, False)
+    ybr = torch.empty(B * T, C, dtype=BF16, device=x.device)
+    out = K.linear(o.view(B * T, C), c_w, c_b, residual=x2, gate=gate, pre_out=ybr)
+    if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
+        ctx.save_for_backward(x2, xn, mean, rstd, qp, kv, o, lse, ybr, ln_w, q_w, c_w, gate)
+        ctx.cfg = (B, T, S, C, n_head, off)
+        _mark(ctx)
+    return out.view(B, T, C)
+
+
+def _xattn_bwd(ctx, dout, dkv, g):
+    """Backward of _xattn_fwd: writes dK / dV into dkv[..., off:off+2C] and fills g at the
+    positions ctx.idx = (x, ln_w, ln_b, q_w, q_b, c_w, c_b, gate) of the caller's inputs."""
+    x2, xn, mean, rstd, qp, kv, o, lse, ybr, ln_w, q_w, c_w, gate = ctx.saved_tensors
+    B, T, S, C, H, off = ctx.cfg
+    ix, iln_w, iln_b, iq_w, iq_b, ic_w, ic_b, igate = ctx.idx
+    P = ctx.params
+    d2 = dout.reshape(B * T, C).to(BF16).contiguous()
+    gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
+    dbr = K.gate_bwd(d2, ybr, gate, gacc)
+    if _need(ctx, igate):
+        g[igate] = gacc.to(gate.dtype).view_as(gate)
+    g[ic_w] = _wgrad(ctx, ic_w, P[ic_w], dbr, o.view(B * T, C), defer=True)
+    g[ic_b] = _bgrad(ctx, ic_b, P[ic_b], dbr, defer=True)
+    do = K.linear_dx(dbr, c_w).view(B, T, C)
+    dqp = torch.empty(B * T, C, dtype=BF16, device=d2.device)
+    K.attn_bwd(do, qp.view(B, T, C), kv[:, :, off:off + C], kv[:, :, off + C:off + 2 * C], o, lse,
+               H, False, dqp.view(B, T, C), dkv[:, :, off:off + C], dkv[:, :, off + C:off + 2 * C])
+    g[iq_w] = _wgrad(ctx, iq_w, P[iq_w], dqp, xn, defer=True)
+    g[iq_b] = _bgrad(ctx, iq_b, P[iq_b], dqp, defer=True)
+    dxn = K.linear_dx(dqp, q_w)
+    dx = torch.empty_like(d2)  # = d2 + LN backward (residual read from d2, no copy)
+    g[iln_w], g[iln_b] = _ln_bwd(ctx, iln_w, iln_b, P[iln_w], P[iln_b], dxn, x2, mean, rstd, dx,
+                                 True, residual=d2)
+    g[ix] = dx.view(B, T, C) if _need(ctx, ix) else None
+
+
+class KVGradSlab:
+    """The [B, S, L*2C] gradient of CrossKVFn's packed output, shared by the L blocks: each
+    block's backward writes its dK / dV columns in place, and the last one to run hands the
+    whole slab to autograd (the others return None), so CrossKVFn.backward — which the engine
+    runs only after all L consumers — sees every column written and no [B, S, L*2C] zeros or
+    slice-gradient adds are ever materialised."""
+
+    def __init__(self, layers):
+        self.layers, self.left, self.buf = layers, layers, None
+
+    def take(self, like):
+        if self.buf is None:
+            self.buf = torch.empty(like.shape, dtype=BF16, device=like.device)
+        return self.buf
+
+    def release(self):
+        self.left -= 1
+        if self.left > 0:
+            return None
+        buf, self.buf, self.left = self.buf, None, self.layers  # (re-armed for retain_graph)
+        return buf
+
+
+class CrossKVFn(torch.autograd.Function):
+    """kv_proj of ALL cross-attention blocks (gpt2_cross-att/model.py:49-50 in each Block)
+    over the same projected CLIP tokens as one GEMM against the stacked weights
+    [L*2C, C] -> packed [B, S, L*2C]; backward: dz as one GEMM (K = L*2C) instead of L
+    dX GEMMs plus L-1 gradient adds, the L weight/bias gradients as deferred problems of
+    the batched launch.  forward(z, slab, w_0, b_0, ..., w_{L-1}, b_{L-1})."""
+
+    @staticmethod
+    def forward(ctx, z, slab, *wb):
+        L = len(wb) // 2
+        B, S, C = z.shape
+        z2 = z.reshape(B * S, C).to(BF16).contiguous()
+        w_all = torch.cat(wb[0::2], 0)
+        kv = K.linear(z2, w_all, torch.cat(wb[1::2], 0))
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(z2, w_all)
+            ctx.cfg = (B, S, C, L)
+            ctx.params = (None, None) + tuple(wb)
+            _mark(ctx)
+        return kv.view(B, S, w_all.shape[0])
+
+    @staticmethod
+    def backward(ctx, dkv):
+        z2, w_all = ctx.saved_tensors
+        B, S, C, L = ctx.cfg
+        d2 = dkv.reshape(B * S, 2 * C * L)
+        if d2.dtype != BF16 or d2.stride(1) != 1:
+            d2 = d2.to(BF16).contiguous()
+        g = [None] * (2 + 2 * L)
+        P = ctx.params
+        for layer in range(L):
+            sl = d2[:, 2 * C * layer:2 * C * (layer + 1)]
+            g[2 + 2 * layer] = _wgrad(ctx, 2 + 2 * layer, P[2 + 2 * layer], sl, z2, defer=True)
+            g[3 + 2 * layer] = _bgrad(ctx, 3 + 2 * layer, P[3 + 2 * layer], sl, defer=True)
+        if _need(ctx, 0):
+            g[0] = K.linear_dx(d2, w_all).view(B, S, C)
+        return tuple(g)
+
+
+class CrossAttnKVFn(torch.autograd.Function):
+    """CrossAttnFn of block `layer` over the packed projection of CrossKVFn (no kv_proj of
+    its own); dK / dV go straight into the shared KVGradSlab."""
+
+    @staticmethod
+    def forward(ctx, x, kv, layer: int, slab, ln_w, ln_b, q_w, q_b, c_w, c_b, gate, n_head: int):
+        C = x.shape[2]
+        out = _xattn_fwd(ctx, x, kv, 2 * C * layer, ln_w, ln_b, q_w, q_b, c_w, c_b, gate, n_head)
+        if any(ctx.needs_input_grad):
+            ctx.slab = slab
+            ctx.params = (None, None, None, None, ln_w, ln_b, q_w, q_b, c_w, c_b)
+            ctx.idx = (0, 4, 5, 6, 7, 8, 9, 10)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        g = [None] * 12
+        kv = ctx.saved_tensors[5]
+        buf = ctx.slab.take(kv)
+        _xattn_bwd(ctx, dout, buf, g)
+        g[1] = ctx.slab.release() if _need(ctx, 1) else None
         return tuple(g)
 
 
