@@ -342,9 +342,10 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
 @pytest.mark.parametrize("b_mn", [0, 1])
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "res_inplace", "bias_act_d", "mul", "dact_erf"])
 @pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 2304), (7992, 776, 192),
-                                   (16384, 768, 384), (300, 128, 192), (8064, 3072, 768)])
+                                   (16384, 768, 384), (300, 128, 192), (8064, 3072, 768),
+                                   (3968, 768, 3072), (4096, 768, 768), (3970, 776, 192)])
 def test_gemm_w4(cuda, b_mn, epi, M, N, K):
-    """Four-wave 192x128 deep-ring kernel (gemm_w4.hip), forced with gvl_gemm_tune(3, 10):
+    """Four-wave 192x128 / 128x128 deep-ring kernel (gemm_w4.hip), forced with gvl_gemm_tune(3, 10):
     the caption decoder's N = 768 shapes (252 tiles, one per CU), ragged M and N (N % 128 != 0),
     several tiles per workgroup with the ring running across tiles (516 tiles), a tile grid
     smaller than the ring, and every epilogue kind."""
@@ -387,7 +388,8 @@ def test_gemm_w4(cuda, b_mn, epi, M, N, K):
         torch.cuda.synchronize()
     finally:
         _lib.lib().gvl_gemm_tune(3, -1)
-    assert name.startswith("gemm_w4_kernel"), name
+    # 128-row tiles (gemm_w4m_kernel) where 192-row ones would fill < 3/4 of the CUs
+    assert name.startswith("gemm_w4m_kernel" if M <= 4096 else "gemm_w4_kernel"), name
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
@@ -532,7 +534,7 @@ def test_gemm_dropout_gate(cuda):
     assert 0.08 < frac < 0.12
 
 
-@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, "gemm_w4_kernel"),
+@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, "gemm_w4m_kernel"),
                                          (4096, 3072, 768, "gemm_pp3_kernel"),
                                          (200, 136, 72, None), (4096, 768, 3072, None)])
 def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
