@@ -94,10 +94,10 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
     }                                                                             \
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
   } while (0)
-#elif GVL_W4_IGLP == 3  // five rounds of {MFMA, read, MFMA, read, MFMA, load, MFMA, write}
+#elif GVL_W4_IGLP == 3  // PA+PB rounds of {MFMA, read, MFMA, read, MFMA, load, MFMA, write}
 #define W4_INTERLEAVE()                                                           \
   do {                                                                            \
-    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) {                            \
+    _Pragma("unroll") for (int q_ = 0; q_ < PA + PB; ++q_) {                      \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
@@ -107,7 +107,8 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                          \
     }                                                                             \
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
+    if constexpr (FM * FN > 4 * (PA + PB))                                        \
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN - 4 * (PA + PB), 0);    \
   } while (0)
 #endif
 #if GVL_W4_IGLP
@@ -133,10 +134,13 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
 #define W4_DIAG_MEM(...) do { __VA_ARGS__; } while (0)
 #endif
 
-template <int NS, bool BMN, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
-  constexpr int BM = W4_BM, BN = W4_BN, NW = 4, FM = 6, FN = 4, P = 3;
+// BM = 192 (6 x 4 fragments per wave) or 128 (4 x 4): the 128-row tile fills the chip when
+// 192-row tiles would leave over a quarter of the CUs idle (3968 / 4096-row caption GEMMs).
+template <int NS, bool BMN, int EPI, int BM>
+__device__ __forceinline__ void gemm_w4_body(const GemmP& p) {
+  constexpr int BN = W4_BN, NW = 4, FM = BM / 32, FN = 4, P = 3;
   static_assert(NS == 3, "ring geometry");
+  static_assert(BM == 192 || BM == 128, "tile rows");
   using SA = Step<BM, false, NW>;
   using SB = Step<BN, BMN, NW>;
   constexpr int SLOT = SA::BYTES + SB::BYTES;
@@ -269,20 +273,42 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
 #undef GVL_W4_LOAD
 }
 
+// Two kernel names (rocprofv3 / the bench timer tell them apart): 192-row and 128-row tiles.
+template <int NS, bool BMN, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmP p) {
+  gemm_w4_body<NS, BMN, EPI, 192>(p);
+}
+template <int NS, bool BMN, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4m_kernel(GemmP p) {
+  gemm_w4_body<NS, BMN, EPI, 128>(p);
+}
+
 #ifndef GVL_W4_NS
 #define GVL_W4_NS 3
 #endif
 
-template <bool BMN, int EPI>
-int launch_w4(const GemmP& p0, hipStream_t s) {
+// Tile walk: XCD-contiguous work items, then groups of `group` tile rows walked row-fastest.
+// GVL_W4_GROUP=1 walks all column tiles of a row block before the next one, so an XCD reads
+// each A row block once (and every column block of B); default: the GEMM-wide group.
+int w4_group(int dflt) {
+  static const int g = [] {
+    const char* e = getenv("GVL_W4_GROUP");
+    return e ? atoi(e) : 0;
+  }();
+  return g > 0 ? g : dflt;
+}
+
+template <bool BMN, int EPI, int BM>
+int launch_w4_bm(const GemmP& p0, hipStream_t s) {
   constexpr int NS = GVL_W4_NS;
   GemmP p = p0;
-  p.tiles_m = (int)((p.M + W4_BM - 1) / W4_BM);
+  p.tiles_m = (int)((p.M + BM - 1) / BM);
   p.tiles_n = (int)((p.N + W4_BN - 1) / W4_BN);
   p.splits = 1;
   p.kper = p.K;
-  constexpr int lds = NS * (W4_BM + W4_BN) * KS * 2;
-  auto kern = gemm_w4_kernel<GVL_W4_NS, BMN, EPI>;
+  p.group = w4_group(p.group);
+  constexpr int lds = NS * (BM + W4_BN) * KS * 2;
+  auto kern = BM == 192 ? gemm_w4_kernel<GVL_W4_NS, BMN, EPI> : gemm_w4m_kernel<GVL_W4_NS, BMN, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -292,6 +318,23 @@ int launch_w4(const GemmP& p0, hipStream_t s) {
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
   gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
   return 0;
+}
+
+// 128-row tiles where 192-row ones fill under 3/4 of the CUs and 128-row ones fill more
+// (GVL_W4_BM128=0: always 192, A/B)
+bool w4_use128(const GemmP& p) {
+  static const bool on = [] {
+    const char* e = getenv("GVL_W4_BM128");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t cus = gvl::num_cus(), tn = (p.N + W4_BN - 1) / W4_BN;
+  const int64_t t192 = (p.M + 191) / 192 * tn, t128 = (p.M + 127) / 128 * tn;
+  return on && t192 * 4 < cus * 3 && t128 > t192 && t128 <= cus;
+}
+
+template <bool BMN, int EPI>
+int launch_w4(const GemmP& p, hipStream_t s) {
+  return w4_use128(p) ? launch_w4_bm<BMN, EPI, 128>(p, s) : launch_w4_bm<BMN, EPI, 192>(p, s);
 }
 
 template <bool BMN>
@@ -349,6 +392,8 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
   // cross-att batched kv_proj dX, K = 18432, do not)
   return tw4 * 5 >= cus * 2 && p.K <= 4096;
 }
+
+bool gemm_w4_rows128(const GemmP& p) { return w4_use128(p); }
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
   return b_mn ? launch_w4_epi<true>(p, s) : launch_w4_epi<false>(p, s);
