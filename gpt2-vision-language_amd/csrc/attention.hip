@@ -125,8 +125,10 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 }
 
 // ------------------------------------------------------------------------------------
+// Short sequences (G = 1, no dropout) compile for 4 waves per SIMD (<= 128 VGPRs, no spill):
+// 4 blocks per CU instead of 3, so the caption decoder's 1536 (b, h) blocks take 1.5 rounds.
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnP p) {
+__global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel(AttnP p) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]

@@ -35,6 +35,15 @@ __global__ __launch_bounds__(LN_FWD_NT) void ln_fwd_kernel(const bf16_t* __restr
   const bf16_t* xr = x + (live ? row : 0) * ldx;
   float v[IT][8];
   float s = 0.f;
+  uint4 wq[IT], bq[IT];  // gamma / beta issued with the row loads (their latency overlaps)
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = (hl + 32 * it) * 8;
+    if (c < C) {
+      wq[it] = *reinterpret_cast<const uint4*>(w + c);
+      bq[it] = *reinterpret_cast<const uint4*>(b + c);
+    }
+  }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int c = (hl + 32 * it) * 8;
@@ -68,8 +77,8 @@ __global__ __launch_bounds__(LN_FWD_NT) void ln_fwd_kernel(const bf16_t* __restr
     const int c = (hl + 32 * it) * 8;
     if (c < C) {
       float wf[8], bf[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
-      unpack8(*reinterpret_cast<const uint4*>(b + c), bf);
+      unpack8(wq[it], wf);
+      unpack8(bq[it], bf);
 #pragma unroll
       for (int r = 0; r < 8; ++r) o[r] = (v[it][r] - mean) * rstd * wf[r] + bf[r];
       *reinterpret_cast<uint4*>(yr + c) = pack8(o);
