@@ -83,7 +83,7 @@ def run_lm(args, world, rank, dev, timer=None):
     model = build_lm(dev)
     model.train()
     opt = _quiet(lambda: model.configure_optimizers(0.1, 6e-4, "cuda"))
-    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb) if world > 1 else None
+    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb, model=model) if world > 1 else None
     batches = [lm_batch(B, T, step=i, rank=rank, device=dev) for i in range(accum)]
     loss_fn = lambda m, b: m(b[0], b[1])[1]
 
@@ -110,7 +110,7 @@ def run_caption(kind, args, world, rank, dev):
     model = build_caption(kind, dev)
     model.train()
     opt = _quiet(lambda: model.configure_optimizers(0.1, 1e-3, "cuda"))
-    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb) if world > 1 else None
+    buckets = GradBuckets(opt, bucket_mb=args.bucket_mb, model=model) if world > 1 else None
     z, x, y, m = caption_batch(B, rank=rank, device=dev)
     if kind == "cross":
         loss_fn = lambda mm, b: mm(b[1], z=pool(b[0]), targets=b[2], target_mask=b[3])[1]

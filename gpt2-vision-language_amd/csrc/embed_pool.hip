@@ -57,6 +57,134 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int64_t* __restrict_
   }
 }
 
+// ---- deterministic embedding backward (ABI v6) -------------------------------------------
+// dwte[v] += sum of dout rows of the tokens with id v, in token order, one fp32 sum per row
+// and ONE bf16 read-modify-write per touched row (no atomics: bit-identical run to run).
+// A chunk of <= EMB_CHUNK tokens is sorted by key (id << 14 | position) with a bitonic sort
+// in LDS by one 1024-thread block; then one wave per sorted slot: the head of each run of
+// equal ids sums its run and updates the row.  Larger inputs run chunk after chunk (the
+// launches are stream-ordered, so a row touched by two chunks is updated in chunk order).
+constexpr int EMB_CHUNK = 16384;  // 64 KiB of keys in LDS
+constexpr uint32_t EMB_BAD = 0xFFFFFFFFu;
+constexpr int EMB_MAXC = 1024;    // 64 lanes x 8 bf16 x 2 slices
+
+__global__ __launch_bounds__(1024) void emb_sort_kernel(const int64_t* __restrict__ idx,
+                                                        int64_t base, int n, int npow,
+                                                        int64_t V, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s[EMB_CHUNK];
+  for (int i = threadIdx.x; i < npow; i += 1024) {
+    uint32_t key = EMB_BAD;
+    if (i < n) {
+      const int64_t id = idx[base + i];
+      if (id >= 0 && id < V) key = ((uint32_t)id << 14) | (uint32_t)i;
+    }
+    s[i] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npow; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (npow >> 1); t += 1024) {
+        const int i = 2 * j * (t / j) + (t % j);
+        const int l = i + j;
+        const uint32_t a = s[i], b = s[l];
+        const bool up = (i & k) == 0;
+        if ((a > b) == up) { s[i] = b; s[l] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < n; i += 1024) out[i] = s[i];
+}
+
+__global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict__ keys, int n,
+                                                       int64_t base, const bf16_t* __restrict__ dout,
+                                                       bf16_t* __restrict__ dwte, int64_t T,
+                                                       int C, int64_t S, int64_t off) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint32_t key = keys[i];
+  if (key == EMB_BAD) return;
+  const uint32_t id = key >> 14;
+  if (i > 0 && (keys[i - 1] >> 14) == id) return;  // not the head of its run
+  const int lane = threadIdx.x & 63;
+  float acc[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
+  for (int j = i; j < n; ++j) {
+    const uint32_t kj = keys[j];
+    if ((kj >> 14) != id || kj == EMB_BAD) break;
+    const int64_t r = base + (int64_t)(kj & 0x3FFFu);
+    const bf16_t* g = dout + ((r / T) * S + off + r % T) * (int64_t)C;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane * 8 + h * 512;
+      if (c < C) {
+        const uint4 u = *reinterpret_cast<const uint4*>(g + c);
+        acc[h][0] += lo_bf(u.x); acc[h][1] += hi_bf(u.x); acc[h][2] += lo_bf(u.y);
+        acc[h][3] += hi_bf(u.y); acc[h][4] += lo_bf(u.z); acc[h][5] += hi_bf(u.z);
+        acc[h][6] += lo_bf(u.w); acc[h][7] += hi_bf(u.w);
+      }
+    }
+  }
+  bf16_t* w = dwte + (int64_t)id * C;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = lane * 8 + h * 512;
+    if (c < C) {
+      const uint4 u = *reinterpret_cast<const uint4*>(w + c);
+      uint4 o;
+      o.x = pack2(lo_bf(u.x) + acc[h][0], hi_bf(u.x) + acc[h][1]);
+      o.y = pack2(lo_bf(u.y) + acc[h][2], hi_bf(u.y) + acc[h][3]);
+      o.z = pack2(lo_bf(u.z) + acc[h][4], hi_bf(u.z) + acc[h][5]);
+      o.w = pack2(lo_bf(u.w) + acc[h][6], hi_bf(u.w) + acc[h][7]);
+      *reinterpret_cast<uint4*>(w + c) = o;
+    }
+  }
+}
+
+// dwpe[t] += sum over sequences g of dout[g*S + off + t], one wave per position t.
+__global__ __launch_bounds__(256) void emb_pos_kernel(const bf16_t* __restrict__ dout,
+                                                       bf16_t* __restrict__ dwpe, int64_t G,
+                                                       int64_t T, int C, int64_t S, int64_t off) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const int lane = threadIdx.x & 63;
+  float acc[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
+  for (int64_t g = 0; g < G; ++g) {
+    const bf16_t* src = dout + (g * S + off + t) * (int64_t)C;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane * 8 + h * 512;
+      if (c < C) {
+        const uint4 u = *reinterpret_cast<const uint4*>(src + c);
+        acc[h][0] += lo_bf(u.x); acc[h][1] += hi_bf(u.x); acc[h][2] += lo_bf(u.y);
+        acc[h][3] += hi_bf(u.y); acc[h][4] += lo_bf(u.z); acc[h][5] += hi_bf(u.z);
+        acc[h][6] += lo_bf(u.w); acc[h][7] += hi_bf(u.w);
+      }
+    }
+  }
+  bf16_t* w = dwpe + t * (int64_t)C;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = lane * 8 + h * 512;
+    if (c < C) {
+      const uint4 u = *reinterpret_cast<const uint4*>(w + c);
+      uint4 o;
+      o.x = pack2(lo_bf(u.x) + acc[h][0], hi_bf(u.x) + acc[h][1]);
+      o.y = pack2(lo_bf(u.y) + acc[h][2], hi_bf(u.y) + acc[h][3]);
+      o.z = pack2(lo_bf(u.z) + acc[h][4], hi_bf(u.z) + acc[h][5]);
+      o.w = pack2(lo_bf(u.w) + acc[h][6], hi_bf(u.w) + acc[h][7]);
+      *reinterpret_cast<uint4*>(w + c) = o;
+    }
+  }
+}
+
 // Pool: block per (b, o), o in [0, 33): o=0 is CLS, o=1+i*8+j the adaptive-avg window
 // rows [floor(i*s/4), ceil((i+1)*s/4)), cols [floor(j*s/8), ceil((j+1)*s/8)); then the
 // 33 tokens are L2-normalised with F.normalize's max(||x||, 1e-12).
@@ -172,6 +300,42 @@ extern "C" int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dw
                      gvl::as_stream(stream), idx, static_cast<const bf16_t*>(dout), dwte_acc,
                      dwpe_acc, n_tokens, T, (int)C, out_rows_per_seq, out_offset, vocab);
   GVL_LAUNCH_CHECK("gvl_embedding_bwd");
+  return 0;
+}
+
+extern "C" int64_t gvl_embedding_bwd_workspace(int64_t n_tokens) {
+  return n_tokens < EMB_CHUNK ? n_tokens : EMB_CHUNK;
+}
+
+extern "C" int gvl_embedding_bwd_det(const int64_t* idx, const void* dout, void* dwte, void* dwpe,
+                                     int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
+                                     int64_t out_rows_per_seq, int64_t out_offset,
+                                     uint32_t* keys, int64_t keys_count, gvl_stream_t stream) {
+  GVL_REQUIRE(C % 8 == 0 && C <= EMB_MAXC && T > 0 && vocab > 0,
+              "gvl_embedding_bwd_det: bad shape (C %% 8 == 0, C <= %d)", EMB_MAXC);
+  GVL_REQUIRE(vocab < (1ll << 18) - 1, "gvl_embedding_bwd_det: vocab must be < 2^18 - 1");
+  GVL_REQUIRE(n_tokens % T == 0, "gvl_embedding_bwd_det: n_tokens must be a multiple of T");
+  if (n_tokens == 0) return 0;
+  hipStream_t s = gvl::as_stream(stream);
+  if (dwte) {
+    GVL_REQUIRE(keys && keys_count >= gvl_embedding_bwd_workspace(n_tokens),
+                "gvl_embedding_bwd_det: key workspace too small");
+    for (int64_t base = 0; base < n_tokens; base += EMB_CHUNK) {
+      const int n = (int)((n_tokens - base) < EMB_CHUNK ? (n_tokens - base) : EMB_CHUNK);
+      int npow = 64;
+      while (npow < n) npow <<= 1;
+      hipLaunchKernelGGL(emb_sort_kernel, dim3(1), dim3(1024), 0, s, idx, base, n, npow, vocab,
+                         keys);
+      hipLaunchKernelGGL(emb_seg_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s,
+                         (const uint32_t*)keys, n, base, static_cast<const bf16_t*>(dout),
+                         static_cast<bf16_t*>(dwte), T, (int)C, out_rows_per_seq, out_offset);
+    }
+  }
+  if (dwpe)
+    hipLaunchKernelGGL(emb_pos_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(dout), static_cast<bf16_t*>(dwpe), n_tokens / T,
+                       T, (int)C, out_rows_per_seq, out_offset);
+  GVL_LAUNCH_CHECK("gvl_embedding_bwd_det");
   return 0;
 }
 

@@ -2,5 +2,10 @@
 Replace those class definitions in the training script with
     from model import CausalSelfAttention, MLP, Block, GPTConfig, GPT
 after putting this directory first on sys.path."""
-import _gvl_path  # noqa: F401
+import os as _os
+import sys as _sys
+
+_PKG = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+if _PKG not in _sys.path:  # the gvl package (gpt2-vision-language_amd/)
+    _sys.path.insert(0, _PKG)
 from gvl.gpt2 import GPT, MLP, Block, CausalSelfAttention, GPTConfig  # noqa: F401

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 5  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 6  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -90,6 +90,9 @@ SIGNATURES = {
                                     c_i64, c_vp]),
     "gvl_embedding_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64,
                                     c_i64, c_vp]),
+    "gvl_embedding_bwd_workspace": (c_i64, [c_i64]),
+    "gvl_embedding_bwd_det": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
+                                        c_i64, c_i64, c_vp, c_i64, c_vp]),
     "gvl_pool_clip": (C.c_int, [c_vp, c_i32, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
     "gvl_pool_clip_ex": (C.c_int, [c_vp, c_i32, c_vp, c_i32, c_i64, c_i64, c_i64, c_i32, c_vp]),
     "gvl_l2_normalize_rows": (C.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),

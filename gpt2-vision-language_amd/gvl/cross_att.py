@@ -50,6 +50,42 @@ class CrossAttention(nn.Module):
         self.n_head = config.n_head
         self.n_embd = config.n_embd
 
+    def forward(self, x, z):
+        """Stand-alone cross-attention (model.py:46-58): c_proj(SDPA(q_proj(x), kv_proj(z))),
+        non-causal, no gate (Block applies tanh(cross_gate) and the residual; the Block path
+        fuses all of it into CrossAttnFn / CrossAttnKVFn)."""
+        q = Fn.LinearFn.apply(x, bf(self.q_proj.weight), bf(self.q_proj.bias))
+        kv = Fn.LinearFn.apply(z, bf(self.kv_proj.weight), bf(self.kv_proj.bias))
+        y = _CrossSDPAFn.apply(q, kv, self.n_head)
+        return Fn.LinearFn.apply(y, bf(self.c_proj.weight), bf(self.c_proj.bias))
+
+
+class _CrossSDPAFn(torch.autograd.Function):
+    """Non-causal attention of q [B, T, C] over a packed kv [B, S, 2C] (K = kv[..., :C],
+    V = kv[..., C:], strided views: no split/transpose copies)."""
+
+    @staticmethod
+    def forward(ctx, q, kv, n_head: int):
+        from . import kernels as K
+        C = q.shape[2]
+        q = q.to(torch.bfloat16).contiguous()
+        kv = kv.to(torch.bfloat16).contiguous()
+        y, lse = K.attn_fwd(q, kv[:, :, :C], kv[:, :, C:], n_head, False)
+        ctx.save_for_backward(q, kv, y, lse)
+        ctx.n_head = n_head
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import kernels as K
+        q, kv, y, lse = ctx.saved_tensors
+        C = q.shape[2]
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        K.attn_bwd(dy.to(torch.bfloat16).contiguous(), q, kv[:, :, :C], kv[:, :, C:], y, lse,
+                   ctx.n_head, False, dq, dkv[:, :, :C], dkv[:, :, C:])
+        return dq, dkv, None
+
 
 class Vision_projector(nn.Module):
     """model.py:78-84."""

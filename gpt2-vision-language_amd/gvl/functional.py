@@ -47,6 +47,22 @@ def _need(ctx, i):
 # device scalar (a sync), so it is skipped inside a hipGraph capture (gvl.graph) and can be
 # turned off with GVL_CHECK_IDS=0.
 CHECK_IDS = os.environ.get("GVL_CHECK_IDS", "1") != "0"
+# The first SYNC_CHECKS checks of a process block on the result (an error raises at the op,
+# like torch).  Later ones stay asynchronous: the device-side verdict is copied into pinned
+# host memory behind an event, and every later call polls the completed verdicts without
+# synchronising, so a bad id raises IndexError one or a few calls after the op that read it
+# (the kernels never read outside their rows meanwhile).  GVL_CHECK_IDS=2: always synchronous.
+SYNC_CHECKS = 1 << 60 if os.environ.get("GVL_CHECK_IDS") == "2" else 16
+_ID_CHECKS = [0]
+_ID_INFLIGHT = []  # (pinned bool, event, what, n)
+
+
+def _poll_id_checks():
+    while _ID_INFLIGHT and _ID_INFLIGHT[0][1].query():
+        flag, _, what, n = _ID_INFLIGHT.pop(0)
+        if bool(flag[0]):
+            _ID_INFLIGHT.clear()
+            raise IndexError(f"gvl: {what} out of range [0, {n}) (detected asynchronously)")
 
 
 def check_index_range(t, n, what, ignore_index=None):
@@ -55,9 +71,18 @@ def check_index_range(t, n, what, ignore_index=None):
     bad = (t < 0) | (t >= n)
     if ignore_index is not None:
         bad &= t != ignore_index
-    if bool(bad.any()):
-        lo, hi = int(t.min()), int(t.max())
-        raise IndexError(f"gvl: {what} out of range [0, {n}) (min {lo}, max {hi})")
+    _ID_CHECKS[0] += 1
+    if not t.is_cuda or _ID_CHECKS[0] <= SYNC_CHECKS:
+        if bool(bad.any()):
+            lo, hi = int(t.min()), int(t.max())
+            raise IndexError(f"gvl: {what} out of range [0, {n}) (min {lo}, max {hi})")
+        return
+    _poll_id_checks()
+    flag = torch.empty(1, dtype=torch.bool, pin_memory=True)
+    flag.copy_(bad.any().view(1), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _ID_INFLIGHT.append((flag, ev, what, n))
 
 
 def pad_vocab(w):
@@ -78,8 +103,8 @@ def pad_vocab(w):
 # "sink": the weight-gradient GEMM adds into it in its epilogue (C = dY^T X + C), bias and
 # LayerNorm gradients use their kernels' accumulate flag, and the Function returns None for
 # that input.  AccumulateGrad then never runs for it, so _ready() notifies the
-# data-parallel bucketing (gvl.dist) in its place.  Tied parameters (wte: embedding +
-# lm_head) keep the autograd path, which sums both uses before one AccumulateGrad.
+# data-parallel bucketing (gvl.dist) in its place.  The tied wte (embedding + lm_head) sinks
+# both uses into its one arena gradient (LMHeadLossFn's GEMM epilogue, EmbedFn's row update).
 FUSE_GRAD_ACC = True
 # MLP GELU: the forward epilogue stores gelu'(x) instead of x (GEMM act 3/4) and the backward
 # multiplies by it (dact 3), so the dX epilogue runs no transcendentals.  0 (GVL_GELU_DERIV=0)
@@ -97,33 +122,80 @@ _READY_HOOKS = []
 # Q-Former / linear bridge launch theirs in place (measured: deferring them is 0.5 % slower).
 # GVL_DEFER_WGRAD=0 launches each one in place.
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
-_PENDING = []          # (param, grad sink, dy2, x2, stream)
-_PENDING_B = []        # (param, grad sink, dy2, stream): bias gradients = column sums of dy2
-_FLUSH_QUEUED = [False]
+# Queue entries are tagged with the autograd graph task that produced them, and every task
+# that defers queues its OWN end-of-backward flush, which runs only that task's entries: two
+# backward passes (two models, two threads, a nested reentrant backward) never consume each
+# other's gradients, and a backward that raises (its final callbacks never run) cannot
+# switch deferral off for later passes.  Its stale entries are dropped by discard_pending(),
+# which gvl.optim.AdamW.zero_grad calls.  Peak memory: the queued (dY, X) operands stay alive
+# until the flush.
+_PENDING = []          # (task, param, grad sink, dy2, x2, stream)
+_PENDING_B = []        # (task, param, grad sink, dy2, stream): bias gradients = column sums of dy2
+_QUEUED = set()        # graph tasks with a flush callback queued
+# Data-parallel overlap (gvl.dist.GradBuckets sets it for the synchronising micro-step):
+# with OVERLAP_BLOCKS[0] = G > 0 every G-th GPT-2 block backward flushes its task's queue in
+# place, so the gradients of the top blocks become final — and their all-reduce buckets
+# launch — while the lower blocks' backward is still running (train_gpt2.py:468-469, DDP's
+# bucketed reducer).  0: one flush at the end of backward (largest batched launches).
+OVERLAP_BLOCKS = [0]
+_BLOCKS_SEEN = {}      # task -> GPT-2 blocks deferred since that task's last flush
 
 
-def flush_wgrads():
-    """Run the queued weight gradients (batched by shape), then notify the grad-ready hooks.
-    Runs by itself at the end of every backward pass that queued any; harmless when empty."""
-    _FLUSH_QUEUED[0] = False
+def _task():
+    return torch._C._current_graph_task_id()
+
+
+def set_overlap_blocks(g: int):
+    """Flush deferred weight gradients every `g` GPT-2 blocks during backward (0: at the end)."""
+    OVERLAP_BLOCKS[0] = max(0, int(g))
+
+
+def discard_pending():
+    """Drop every queued deferred gradient (left behind by a backward that raised)."""
+    _PENDING.clear()
+    _PENDING_B.clear()
+    _QUEUED.clear()
+    _BLOCKS_SEEN.clear()
+
+
+def _take(lst, task):
+    if task is None:
+        out = list(lst)
+        lst.clear()
+        return out
+    out = [e for e in lst if e[0] == task]
+    if out:
+        lst[:] = [e for e in lst if e[0] != task]
+    return out
+
+
+def _dkey(d):
+    return (d.data_ptr(), tuple(d.shape), d.stride(0))
+
+
+def flush_wgrads(task=None):
+    """Run the queued weight gradients of graph task `task` (every task when None) batched by
+    shape, then notify the grad-ready hooks.  Runs by itself at the end of every backward pass
+    that queued any; harmless when empty."""
+    pend = [e[1:] for e in _take(_PENDING, task)]
+    pend_b = [e[1:] for e in _take(_PENDING_B, task)]
+    _BLOCKS_SEEN.pop(task, None)
     # a bias gradient over the same dY as a queued weight gradient rides in that batched GEMM
-    # (gvl_gemm_batched_dbias: row sums of dY^T from the same operand tiles)
+    # (gvl_gemm_batched_dbias: row sums of dY^T from the same operand tiles); each bias pairs
+    # with ONE weight gradient (popped when used), so a dY shared by two weight gradients
+    # never gets its bias fused twice
     paired = {}
-    if _PENDING_B and _PENDING:
-        wkeys = {(d.data_ptr(), tuple(d.shape), d.stride(0)) for _, _, d, _, _ in _PENDING}
-        rest = []
-        for p, g, dy2, st in _PENDING_B:
-            k = (dy2.data_ptr(), tuple(dy2.shape), dy2.stride(0))
+    rest_b = []
+    if pend_b and pend:
+        wkeys = {_dkey(d) for _, _, d, _, _ in pend}
+        for p, g, dy2, st in pend_b:
+            k = _dkey(dy2)
             if k in wkeys and k not in paired:
                 paired[k] = (p, g)
             else:
-                rest.append((p, g, dy2, st))
-        _PENDING_B[:] = rest
-    if not _PENDING:
-        pend = []
+                rest_b.append((p, g, dy2, st))
     else:
-        pend = list(_PENDING)
-        _PENDING.clear()
+        rest_b = pend_b
     groups = {}
     for p, g, dy2, x2, st in pend:
         key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
@@ -133,7 +205,7 @@ def flush_wgrads():
         with torch.cuda.stream(key[-1]):
             for i in range(0, len(items), 16):
                 chunk = items[i:i + 16]
-                bias = [paired.get((d.data_ptr(), tuple(d.shape), d.stride(0))) for _, _, d, _ in chunk]
+                bias = [paired.pop(_dkey(d), None) for _, _, d, _ in chunk]
                 fused = all(b is not None for b in bias) and K.gemm_batched(
                     [(dy2, x2, g, True) for _, g, dy2, x2 in chunk], a_mn=True, b_mn=True,
                     dbias=[b[1] for b in bias])
@@ -142,17 +214,17 @@ def flush_wgrads():
                                    b_mn=True)
                     for (_, _, d, _), b in zip(chunk, bias):
                         if b is not None:
-                            _PENDING_B.append((b[0], b[1], d, key[-1]))
+                            rest_b.append((b[0], b[1], d, key[-1]))
                 for p, *_ in chunk:
                     _ready(p)
                 if fused:
                     for b in bias:
                         _ready(b[0])
-    if _PENDING_B:
-        pb = list(_PENDING_B)
-        _PENDING_B.clear()
+    for k, (p, g) in paired.items():  # (unreachable unless a weight entry vanished)
+        raise RuntimeError(f"gvl: unpaired deferred bias gradient {k}")
+    if rest_b:
         bgroups = {}
-        for p, g, dy2, st in pb:
+        for p, g, dy2, st in rest_b:
             bgroups.setdefault((tuple(dy2.shape), dy2.stride(0), dy2.device, st), []).append((p, g, dy2))
         for key, items in bgroups.items():
             with torch.cuda.stream(key[-1]):
@@ -164,14 +236,34 @@ def flush_wgrads():
                         _ready(p)
 
 
+def _final_flush(task):
+    _QUEUED.discard(task)
+    flush_wgrads(task)
+
+
 def _defer_wgrad(p, g, dy2, x2):
+    task = _task()
     if x2 is None:  # bias gradient
-        _PENDING_B.append((p, g, dy2, torch.cuda.current_stream(dy2.device)))
+        _PENDING_B.append((task, p, g, dy2, torch.cuda.current_stream(dy2.device)))
     else:
-        _PENDING.append((p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
-    if not _FLUSH_QUEUED[0]:
-        _FLUSH_QUEUED[0] = True
-        torch.autograd.Variable._execution_engine.queue_callback(flush_wgrads)
+        _PENDING.append((task, p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
+    if task not in _QUEUED:
+        _QUEUED.add(task)
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _final_flush(task))
+
+
+def _block_done():
+    """End of one GPT-2 block's backward: with data-parallel overlap on, flush this task's
+    queue every OVERLAP_BLOCKS blocks."""
+    G = OVERLAP_BLOCKS[0]
+    if G <= 0 or not DEFER_WGRAD:
+        return
+    task = _task()
+    n = _BLOCKS_SEEN.get(task, 0) + 1
+    if n >= G:
+        flush_wgrads(task)
+    else:
+        _BLOCKS_SEEN[task] = n
 
 
 def register_grad_ready_hook(fn):
@@ -340,6 +432,7 @@ class GPTBlockFn(torch.autograd.Function):
         dx = torch.empty_like(dxm)  # dxm stays intact: the (deferred) c_proj dW reads it
         g[1], g[2] = _ln_bwd(ctx, 1, 2, P[1], P[2], dxn1, x2, m1, r1, dx, True, residual=dxm)
         g[0] = dx.view(B, T, C) if _need(ctx, 0) else None
+        _block_done()
         return tuple(g)
 
 
@@ -659,9 +752,15 @@ class KVGradSlab:
     slice-gradient adds are ever materialised."""
 
     def __init__(self, layers):
-        self.layers, self.left, self.buf = layers, layers, None
+        self.layers, self.left, self.buf, self.task = layers, layers, None, None
 
     def take(self, like):
+        # re-armed per autograd graph task: a backward that stopped part-way (raised, or
+        # torch.autograd.grad to an intermediate output) leaves no half-counted state for the
+        # next backward over the same (retained) graph
+        task = _task()
+        if self.task != task:
+            self.task, self.left, self.buf = task, self.layers, None
         if self.buf is None:
             self.buf = torch.empty(like.shape, dtype=BF16, device=like.device)
         return self.buf
@@ -670,7 +769,7 @@ class KVGradSlab:
         self.left -= 1
         if self.left > 0:
             return None
-        buf, self.buf, self.left = self.buf, None, self.layers  # (re-armed for retain_graph)
+        buf, self.buf, self.left, self.task = self.buf, None, self.layers, None
         return buf
 
 
@@ -740,7 +839,12 @@ class CrossAttnKVFn(torch.autograd.Function):
 # ------------------------------------------------------------------------ embeddings
 class EmbedFn(torch.autograd.Function):
     """wte(idx) + wpe(arange(T)) written at row offset `off` of a [B, S, C] buffer whose
-    first `off` rows per sequence are `prefix` (the caption image tokens; may be None)."""
+    first `off` rows per sequence are `prefix` (the caption image tokens; may be None).
+
+    Backward: the deterministic per-id / per-position sums (gvl_embedding_bwd_det, no
+    atomics) accumulate straight into arena-sink gradients; the tied wte therefore gets the
+    lm_head weight gradient (LMHeadLossFn, GEMM epilogue C += dl^T x) and this row update in
+    ONE bf16 buffer, with no [V, C] temporary, cast or autograd add per micro-step."""
 
     @staticmethod
     def forward(ctx, idx, wte, wpe, prefix=None):
@@ -756,6 +860,8 @@ class EmbedFn(torch.autograd.Function):
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(idx)
             ctx.cfg = (B, T, C, M, S, wte.shape[0], wpe.shape[0], wte.dtype, wpe.dtype)
+            ctx.params = (None, wte, wpe)
+            _mark(ctx)
         return out
 
     @staticmethod
@@ -765,13 +871,22 @@ class EmbedFn(torch.autograd.Function):
         dout = dout.to(BF16).contiguous()
         dwte = dwpe = dprefix = None
         if _need(ctx, 1) or _need(ctx, 2):
-            acc_te = torch.zeros(V, C, dtype=torch.float32, device=dout.device) if _need(ctx, 1) else None
-            acc_pe = torch.zeros(P, C, dtype=torch.float32, device=dout.device) if _need(ctx, 2) else None
-            K.embedding_bwd(idx, dout, acc_te, acc_pe, T, S, M, C, V)
-            if acc_te is not None:
-                dwte = acc_te.to(dt_te)
-            if acc_pe is not None:
-                dwpe = acc_pe.to(dt_pe)
+            wte, wpe = ctx.params[1], ctx.params[2]
+            gte = _sink(wte, ctx) if _need(ctx, 1) else None
+            gpe = _sink(wpe, ctx) if _need(ctx, 2) else None
+            tte = gte if gte is not None else (
+                torch.zeros(V, C, dtype=BF16, device=dout.device) if _need(ctx, 1) else None)
+            tpe = gpe if gpe is not None else (
+                torch.zeros(P, C, dtype=BF16, device=dout.device) if _need(ctx, 2) else None)
+            K.embedding_bwd_det(idx, dout, tte, tpe, T, S, M, C, V)
+            if gte is not None:
+                _ready(wte)
+            elif tte is not None:
+                dwte = tte if dt_te == BF16 else tte.to(dt_te)
+            if gpe is not None:
+                _ready(wpe)
+            elif tpe is not None:
+                dwpe = tpe if dt_pe == BF16 else tpe.to(dt_pe)
         if M > 0 and _need(ctx, 3):
             dprefix = dout[:, :M]
         return None, dwte, dwpe, dprefix
@@ -797,6 +912,9 @@ class LMHeadLossFn(torch.autograd.Function):
         vocab = V if vocab is None else vocab
         check_index_range(targets, vocab, "target", ignore_index=-100)
         need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        if need:
+            ctx.params = (None, w)
+            _mark(ctx)
         out, dl = K.cross_entropy(logits, targets, rows_per_group=T, group_stride=S,
                                   row_offset=row_offset, mask=mask, mask_mode=mask_mode,
                                   want_grad=need, vocab=vocab)
@@ -829,7 +947,12 @@ class LMHeadLossFn(torch.autograd.Function):
                 xt = x2
             else:
                 xt = x2.view(B, S, C)[:, off:off + T].reshape(B * T, C).contiguous()
-            dw = K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale)
+            g = _sink(ctx.params[1], ctx)  # the tied wte's arena gradient: C += dl^T x
+            if g is not None:
+                K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale, out=g, residual=g)
+                _ready(ctx.params[1])
+            else:
+                dw = K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale)
         return dx, dw, None, None, None, None, None
 
 

@@ -167,6 +167,9 @@ class GPT(nn.Module):
         ))
         self.lm_head = nn.Linear(config.n_embd, config.vocab_size, bias=False)
         self.transformer.wte.weight = self.lm_head.weight
+        # tied: its gradient is final only after both the lm_head and the embedding backward
+        # (gvl.dist.GradBuckets reduces it at the end of backward)
+        self.lm_head.weight._gvl_tied = True
         self.apply(lambda m: init_gpt_weights(m, self.config.n_layer))
 
     def forward(self, idx, targets=None):

@@ -13,13 +13,19 @@ with a single launch.  What changes between steps stays correct under replay:
   * inputs are the captured tensors: feed new data with `copy_` into `micro_batches`
     (static buffers), as a reference loop's next_batch() would.
 
-Data-parallel steps (world > 1, `buckets` given) are captured in two segments around the
-exchange: graph A = zero_grad + every micro-step's forward/backward (the bucket hooks stay
-idle), then ONE eager RCCL AVG all-reduce of the whole grad arena plus the scalar loss
-all-reduce on the current stream, then graph B = grad-norm + clip + AdamW.  No collective is
-captured (so replay cannot deadlock on a rank that captured differently); the exchange loses
-its overlap with the last backward, which costs ~2(N-1)/N x 39 MB (Q-Former) / 249 MB (LM)
-over xGMI per optimizer step — small next to the step.
+Data-parallel steps (world > 1, `buckets` given) keep the gradient exchange overlapped
+with backward without capturing any collective (so a replay cannot deadlock on a rank that
+captured differently): the last micro-step's backward runs in segments
+(gvl.dist.BackwardSegments, cut every few GPT-2 blocks / between Q-Former layers), each
+segment captured as its own graph in one shared memory pool:
+
+    A_0 = zero_grad + micro-steps 0..n-2 + the last forward + backward of the top segment
+    A_j = backward of segment j (its deferred weight gradients flush at its end)
+    B   = grad-norm + clip + AdamW
+
+Replay: A_0, then for each segment the all-reduces of the buckets the previous segment
+finalised (recorded at capture time) are issued on RCCL's stream before A_j is replayed,
+so they run while A_j's kernels do; the rest, the scalar loss all-reduce and B follow.
 """
 from __future__ import annotations
 
@@ -28,14 +34,16 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
-from .dist import _avg, all_reduce_mean_
-from .train import StepResult, accumulate, finish, train_step
+from .dist import all_reduce_mean_
+from .train import StepResult, finish, train_step
 
 
 class GraphedStep:
     def __init__(self, model, optimizer, micro_batches, loss_fn, lr, *, max_norm: float = 1.0,
-                 warmup: int = 2, buckets=None, process_group=None, segmented=None):
-        """Runs `warmup` eager steps at `lr` on a side stream (allocator + kernel caches
+                 warmup: int = 2, buckets=None, process_group=None, segmented=None,
+                 cuts=None):
+        """`cuts`: modules where the DP backward is segmented (default
+        gvl.dist.segment_cuts(model)).  Runs `warmup` eager steps at `lr` on a side stream (allocator + kernel caches
         warm, the optimizer arenas built), then captures one step.  Hyper-parameters other
         than lr (betas, eps, weight_decay, max_norm) are frozen into the graph."""
         self.model, self.opt = model, optimizer
@@ -63,15 +71,57 @@ class GraphedStep:
                 self.seed_off.add_(1)
             self.result = StepResult(res.loss, res.norm)
             return
-        buckets.set_sync(False)  # hooks idle inside the capture: no collective is recorded
-        self.graph_a = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_a):
-            loss = accumulate(model, optimizer, micro_batches, loss_fn, None)
-        self.graph_b = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_b):
-            norm = finish(optimizer, None, max_norm)
-            self.seed_off.add_(1)
-        self.result = StepResult(loss, norm)
+        self._capture_dp(model, optimizer, micro_batches, loss_fn, max_norm, buckets, cuts)
+
+    def _capture_dp(self, model, optimizer, micro_batches, loss_fn, max_norm, buckets, cuts):
+        from .dist import BackwardSegments, segment_cuts
+        segs = BackwardSegments(segment_cuts(model) if cuts is None else cuts)
+        accum = len(micro_batches)
+        self.graphs, self.logs = [], []
+        side = torch.cuda.Stream()
+        torch.cuda.synchronize()
+
+        def begin():
+            g = torch.cuda.CUDAGraph()
+            pool = self.graphs[0].pool() if self.graphs else None
+            g.capture_begin(*(() if pool is None else (pool,)))
+            self.graphs.append(g)
+            self.logs.append([])
+            buckets.capture_log = self.logs[-1]
+
+        try:
+            with torch.cuda.stream(side):
+                begin()
+                buckets.set_sync(False)
+                optimizer.zero_grad()
+                loss_accum = None
+                for i, batch in enumerate(micro_batches):
+                    last = i == accum - 1
+                    if last:
+                        buckets.set_sync(True)
+                        segs.arm(True)
+                    loss = loss_fn(model, batch) / accum
+                    la = loss.detach().float()
+                    loss_accum = la if loss_accum is None else loss_accum + la
+                    if last:
+                        segs.backward(loss, between=lambda j: (self.graphs[-1].capture_end(),
+                                                               begin()))
+                    else:
+                        loss.backward()
+                buckets.wait()  # (capture mode: only records the buckets still pending)
+                self.graphs[-1].capture_end()
+                buckets.capture_log = None
+                self.graph_b = torch.cuda.CUDAGraph()
+                self.graph_b.capture_begin(self.graphs[0].pool())
+                norm = finish(optimizer, None, max_norm)
+                self.seed_off.add_(1)
+                self.graph_b.capture_end()
+        finally:
+            buckets.capture_log = None
+            segs.remove()
+        torch.cuda.current_stream().wait_stream(side)
+        self.buckets = buckets
+        self.result = StepResult(loss_accum, norm)
 
     def __call__(self, lr) -> StepResult:
         """One optimizer step at learning rate `lr` (every param group, like
@@ -82,8 +132,13 @@ class GraphedStep:
         if not self.dp:
             self.graph.replay()
             return self.result
-        self.graph_a.replay()
-        _avg(self.opt.grad_arena, self.pg, async_op=False)
+        bk = self.buckets
+        self.graphs[0].replay()
+        for log, g in zip(self.logs[:-1], self.graphs[1:]):
+            bk.launch_logged(log)  # overlaps the next segment's replay
+            g.replay()
+        bk.launch_logged(self.logs[-1])
+        bk.join()
         all_reduce_mean_(self.result.loss, self.pg)
         self.graph_b.replay()
         return self.result

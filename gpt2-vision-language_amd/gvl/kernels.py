@@ -434,6 +434,32 @@ def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset
                                       out_offset, _stream()), "gvl_embedding_bwd")
 
 
+_EMB_KEYS = {}
+
+
+def embedding_bwd_det(idx, dout, dwte, dwpe, T, out_rows_per_seq, out_offset, C_, V):
+    """Deterministic embedding backward into bf16 gradients, accumulating in place
+    (gvl_embedding_bwd_det): dwte [V, C] += per-id row sums, dwpe [P, C] += per-position sums."""
+    _dev(idx, dout)
+    idx = idx.contiguous()
+    n = idx.numel()
+    for t in (dwte, dwpe):
+        if t is not None and (t.dtype != BF16 or not t.is_contiguous()):
+            raise TypeError("gvl.embedding_bwd_det: gradients must be contiguous bf16")
+    keys = None
+    if dwte is not None:
+        need = int(_L().gvl_embedding_bwd_workspace(n))
+        key = (dout.device, torch.cuda.current_stream(dout.device).cuda_stream)
+        keys = _EMB_KEYS.get(key)
+        if keys is None or keys.numel() < need:
+            keys = torch.empty(max(need, 1), dtype=torch.int32, device=dout.device)
+            _EMB_KEYS[key] = keys
+    _lib.check(_L().gvl_embedding_bwd_det(idx.data_ptr(), dout.data_ptr(), _p(dwte), _p(dwpe), n,
+                                          T, C_, V, out_rows_per_seq, out_offset, _p(keys),
+                                          0 if keys is None else keys.numel(), _stream()),
+               "gvl_embedding_bwd_det")
+
+
 # ------------------------------------------------------------------------------- pool
 def pool_clip(tokens, out_dtype=None, normalize=True):
     """[B, 1+s*s, D] -> [B, 33, D]: CLS + adaptive-avg (4,8) (+ L2 normalise)."""

@@ -83,6 +83,8 @@ class AdamW(torch.optim.Optimizer):
                 mview.copy_(st["master"].to(device=dev, dtype=F32).view_as(p) if "master" in st
                             else p.data.float())
                 st["master"] = mview
+            else:
+                st.pop("master", None)  # a stale fp32-master snapshot must not be resaved
             p.data = view
             gview = garena[o:o + n].view_as(p)
             if p.grad is not None:
@@ -149,6 +151,8 @@ class AdamW(torch.optim.Optimizer):
         """Zero the grad arena in one memset; grads stay arena views (set_to_none ignored)."""
         if self._arena is None:
             self._build()
+        from . import functional as F
+        F.discard_pending()  # deferred gradients left by a backward that raised
         self._arena["g"].zero_()
         self._sync_grads()
 
@@ -204,6 +208,8 @@ class AdamW(torch.optim.Optimizer):
         if self._arena is not None:
             for p in self._arena["params"]:
                 self.state[p]["step"].fill_(self._step_count)
+                if not self.master_weights:
+                    self.state[p].pop("master", None)
         return super().state_dict()
 
     def load_state_dict(self, state_dict):
@@ -234,6 +240,8 @@ class AdamW(torch.optim.Optimizer):
             keys = [("exp_avg", a["m"]), ("exp_avg_sq", a["v"])]
             if a["w"] is not None:
                 keys.append(("master", a["w"]))
+            else:
+                st.pop("master", None)
             for key, arena in keys:
                 view = arena[o:o + n].view_as(p)
                 if key in st and st[key].data_ptr() != view.data_ptr():

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 5
+#define GVL_ABI_VERSION 6
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -218,6 +218,19 @@ int gvl_embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void
 int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc, float* dwpe_acc,
                       int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
                       int64_t out_rows_per_seq, int64_t out_offset, gvl_stream_t stream);
+/* ABI v6: deterministic embedding backward accumulated IN PLACE into bf16 gradients:
+ * dwte[v] += sum of dout[row(r)] over the tokens r with idx[r] == v (summed in fp32 in token
+ * order, one bf16 read-modify-write per touched row — no atomics, bit-identical run to run);
+ * dwpe[t] += sum over sequences of dout[row(seq, t)].  Either pointer may be NULL.  The tied
+ * wte's gradient is the lm_head weight gradient plus this (train_gpt2.py:114-117, :108 tying);
+ * both accumulate into one arena gradient.  `keys`: uint32 scratch of
+ * gvl_embedding_bwd_workspace(n_tokens) entries.  C % 8 == 0, C <= 1024, vocab < 2^18 - 1,
+ * n_tokens % T == 0; ids outside [0, vocab) contribute nothing. */
+int64_t gvl_embedding_bwd_workspace(int64_t n_tokens);
+int gvl_embedding_bwd_det(const int64_t* idx, const void* dout, void* dwte, void* dwpe,
+                          int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
+                          int64_t out_rows_per_seq, int64_t out_offset, uint32_t* keys,
+                          int64_t keys_count, gvl_stream_t stream);
 
 /* ------------------------------------------------------------------------- */
 /* CLIP token pooling: [CLS] + adaptive_avg_pool2d(side x side -> 4 x 8) + L2 normalise

@@ -204,3 +204,136 @@ def test_gloo_buckets_with_fused_sinks_and_sync_toggle():
     assert float(loss_ref) == pytest.approx(out[0][4], rel=1e-6)
     for a, b in zip(m.parameters(), out[0][5]):
         assert torch.allclose(a.detach(), torch.from_numpy(b), atol=1e-6)
+
+
+# ------------------------------------------------------------ overlap with backward (A12)
+class _Res(torch.nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.lin = torch.nn.Linear(d, d)
+
+    def forward(self, x):  # residual inside the block, like GPTBlockFn
+        return x + torch.nn.functional.gelu(self.lin(x))
+
+
+class _Stack(torch.nn.Module):
+    """A decoder-shaped toy: input layer, `n` residual blocks, head — so bucket readiness
+    and segment cuts follow the same module order as GPT.transformer.h."""
+
+    def __init__(self, n=6, d=32):
+        super().__init__()
+        torch.manual_seed(0)
+        self.inp = torch.nn.Linear(16, d)
+        self.h = torch.nn.ModuleList([_Res(d) for _ in range(n)])
+        self.head = torch.nn.Linear(d, 4)
+
+    def forward(self, x):
+        x = self.inp(x)
+        for blk in self.h:
+            x = blk(x)
+        return self.head(x)
+
+
+class GroupedArenaSGD(ArenaSGD):
+    """Arena laid out like gvl.optim.AdamW: the >=2-D (decay) group first, then the biases,
+    each group in module order."""
+
+    def __init__(self, params, lr):
+        ps = list(params)
+        torch.optim.SGD.__init__(self, [{"params": [p for p in ps if p.dim() >= 2]},
+                                        {"params": [p for p in ps if p.dim() < 2]}], lr=lr)
+        order = [p for g in self.param_groups for p in g["params"]]
+        self._layout, off = [], 0
+        for p in order:
+            self._layout.append((p, off, p.numel()))
+            off += (p.numel() + 7) // 8 * 8
+        self._g = torch.zeros(off)
+        for p, o, n in self._layout:
+            p.grad = self._g[o:o + n].view_as(p)
+
+
+def _worker_overlap(rank, world, port, q, segmented):
+    try:
+        _overlap_body(rank, world, port, q, segmented)
+    except BaseException as e:  # report instead of leaving the parent waiting
+        q.put((rank, repr(e)))
+        raise
+
+
+def _overlap_body(rank, world, port, q, segmented):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gvl.dist as D
+    events = []
+    real = D._avg
+
+    def logging_avg(t, pg, async_op):
+        events.append(("bucket", t.data_ptr()))
+        return real(t, pg, async_op)
+    D._avg = logging_avg
+    m = _Stack()
+    def mark(i):
+        def hook(mod, a, out):
+            out.register_hook(lambda g: events.append(("bwd", i)))
+        return hook
+    for i, blk in enumerate(m.h):
+        blk.register_forward_hook(mark(i))
+    opt = GroupedArenaSGD(m.parameters(), lr=0.1)
+    # one bucket per ~block (32x32 weight + bias = 1056 params)
+    bk = D.GradBuckets(opt, bucket_mb=1056 * 4 / (1024 * 1024), model=m)
+    x, y = _data(rank, 8)
+    bk.set_sync(True)
+    if segmented:
+        segs = D.BackwardSegments([m.h[2], m.h[4]])
+        segs.arm(True)
+        loss = ((m(x) - y) ** 2).mean()
+        n = segs.backward(loss, between=lambda j: events.append(("between", j)))
+        assert n == 3
+    else:
+        loss = ((m(x) - y) ** 2).mean()
+        loss.backward()
+    bk.wait()
+    first_bucket_params = [n for n, p in m.named_parameters() if any(p is b for b in bk.buckets[0][1])]
+    q.put((rank, events, [len(r) for r, _ in bk.buckets], first_bucket_params,
+           [p.grad.clone().numpy() for p in m.parameters()]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("segmented", [False, True])
+def test_gloo_buckets_overlap_backward(segmented):
+    """The first gradient bucket (the top block's weight AND bias, two arena runs of the
+    decay-grouped arena) is all-reduced before the backward of the lowest blocks starts —
+    eagerly, and through BackwardSegments (the captured DP step's segment order) — and the
+    reduced gradients equal the mean over ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap, args=(r, 2, port, q, segmented)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=150) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+    assert all(len(o) == 5 for o in out), out
+    for rank, events, runs, first, grads in out:
+        kinds = [e[0] if e[0] != "bwd" else f"bwd{e[1]}" for e in events]
+        assert "head.weight" in first and "head.bias" in first, first
+        assert runs[0] == 2, runs  # weight run + bias run of the grouped arena
+        first_b = kinds.index("bucket")
+        assert first_b < kinds.index("bwd0"), kinds
+        assert first_b < kinds.index("bwd3"), kinds
+        if segmented:
+            assert kinds.index("between") < kinds.index("bwd3"), kinds
+    # reduced gradients: identical on both ranks and equal to the mean of local gradients
+    m = _Stack()
+    ref = [torch.zeros_like(p) for p in m.parameters()]
+    for r in range(2):
+        m.zero_grad()
+        x, y = _data(r, 8)
+        ((m(x) - y) ** 2).mean().backward()
+        for a, p in zip(ref, m.parameters()):
+            a += p.grad / 2
+    for g0, g1, r in zip(out[0][4], out[1][4], ref):
+        assert torch.allclose(torch.from_numpy(g0), torch.from_numpy(g1))
+        assert torch.allclose(torch.from_numpy(g0), r, atol=1e-6)

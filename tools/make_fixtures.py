@@ -605,6 +605,85 @@ def fixture_greedy(g2, lin, qf, xa, meta):
     np.savez_compressed(os.path.join(OUT, "greedy.npz"), **out)
 
 
+BENCH_CAP_B = 128   # bench.py caption batch
+BENCH_LM_B = 16     # bench.py LM micro-batch (configs[1])
+
+
+def _grads_out(model, names, out, pre):
+    params = dict(model.named_parameters())
+    sq = 0.0
+    for n in names:
+        g = params[n].grad
+        sample_tensor(n, g, out, f"{pre}grad:{n}")
+        sq += float((g.double() ** 2).sum())
+    out[pre + "gradnorm"] = np.array(np.sqrt(sq))
+
+
+def fixture_bench_shapes(g2, lin, qf, xa, meta):
+    """One forward+backward of the reference at EXACTLY the bench's shapes (round 3): the
+    caption models at B=128 (8,064 / 3,968 / 4,096-row GEMMs, the four-wave kernels' routing)
+    and the LM at one B=16 x 1024 micro-step (M = 16,384 dX GEMMs, K = 16,384 batched weight
+    gradients).  The reference runs on the bf16-valued recipe weights in fp32 math (the
+    `mp` loop of train_ref), so the comparison isolates the GPU path's compute error; the
+    loss at the fp32 recipe weights is stored too (`loss_fp32w`, the north-star 1e-4 bar)."""
+    out = {}
+    torch.set_grad_enabled(True)
+    for kind, mod in (("qformer", qf), ("linear", lin)):
+        lm = mod.GPT_previous(mod.GPTConfig(vocab_size=50304, block_size=1024))
+        model = set_recipe(mod.GPT_Caption(enc_dim=768, lm=lm, m_vis_tokens=32))
+        model.eval()
+        z_raw, x, yy, mask = inputs_caption(BENCH_CAP_B, 257, 768, 31, 50257, 1313)
+        labels = yy.masked_fill(~mask, -100)
+        z = mod.pool_clip_197_to_33_avg_with_cls(z_raw)
+        with torch.no_grad():
+            out[f"{kind}_loss_fp32w"] = np.array(float(model(z, x, labels=labels)[1]))
+        round_bf16_(model)
+        _, loss = model(z, x, labels=labels)
+        loss.backward()
+        names = [n for n, p in model.named_parameters() if p.requires_grad]
+        meta[f"bench_{kind}_trainable"] = names
+        out[f"{kind}_loss"] = np.array(float(loss))
+        _grads_out(model, names, out, f"{kind}_")
+        out[f"{kind}_x"], out[f"{kind}_labels"] = x.numpy(), labels.numpy()
+        print(kind, float(loss), out[f"{kind}_loss_fp32w"], out[f"{kind}_gradnorm"], flush=True)
+        del model, lm, loss
+    model = set_recipe(xa.GPT(xa.GPTConfig(vocab_size=50304, block_size=1024)))
+    z_raw, x, yy, mask = inputs_caption(BENCH_CAP_B, 257, 768, 31, 50257, 1414)
+    z = xa.pool_clip_197_to_33_avg_with_cls(z_raw)
+    with torch.no_grad():
+        out["cross_loss_fp32w"] = np.array(float(model(x, z=z, targets=yy, target_mask=mask)[1]))
+    round_bf16_(model)
+    _, loss = model(x, z=z, targets=yy, target_mask=mask)
+    loss.backward()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    meta["bench_cross_trainable"] = names
+    out["cross_loss"] = np.array(float(loss))
+    _grads_out(model, names, out, "cross_")
+    out["cross_x"], out["cross_y"], out["cross_mask"] = x.numpy(), yy.numpy(), mask.numpy()
+    print("cross", float(loss), out["cross_loss_fp32w"], out["cross_gradnorm"], flush=True)
+    del model, loss
+    out["z_seeds"] = np.array([1313, 1414])
+    out["cap_batch"] = np.array(BENCH_CAP_B)
+    # LM: one micro-step of the bench's B=16 x 1024 (the x, y windows regenerate on the box
+    # from the recipe id stream, seed 4040)
+    cfg = g2["GPTConfig"](vocab_size=50304)
+    model = set_recipe(g2["GPT"](cfg))
+    x, y = inputs_lm(BENCH_LM_B, 1024, 50257, 4040)
+    with torch.no_grad():
+        out["lm_loss_fp32w"] = np.array(float(model(x, y)[1]))
+    round_bf16_(model)
+    _, loss = model(x, y)
+    loss.backward()
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    meta["bench_lm_trainable"] = names
+    out["lm_loss"] = np.array(float(loss))
+    _grads_out(model, names, out, "lm_")
+    out["lm_seed"] = np.array(4040)
+    out["lm_batch"] = np.array(BENCH_LM_B)
+    print("lm", float(loss), out["lm_loss_fp32w"], out["lm_gradnorm"], flush=True)
+    np.savez_compressed(os.path.join(OUT, "bench_shapes.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also the 124M scalar fixtures")
@@ -627,7 +706,8 @@ def main():
         sets = {"full_train": lambda: fixture_full_train(g2, lin, qf, xa, meta),
                 "accum": lambda: fixture_accum(g2, qf, meta),
                 "edge": lambda: fixture_edge(lin, qf, xa, meta),
-                "greedy": lambda: fixture_greedy(g2, lin, qf, xa, meta)}
+                "greedy": lambda: fixture_greedy(g2, lin, qf, xa, meta),
+                "bench_shapes": lambda: fixture_bench_shapes(g2, lin, qf, xa, meta)}
         for name in args.only.split(","):
             sets[name]()
         with open(mpath, "w") as f:
