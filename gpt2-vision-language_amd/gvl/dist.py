@@ -47,8 +47,16 @@ def _is_nccl(pg):
 def _avg(t, pg, async_op):
     if _is_nccl(pg):
         return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=pg, async_op=async_op)
+    # gloo (CPU tests; GPU tensors in the two-ranks-on-one-GPU tests): its host-staged copy
+    # of a device tensor is not reliably ordered behind kernels queued on the caller's stream
+    # (measured: deferred weight gradients reduced before they were written), so the device
+    # is drained around it — gloo is never the production path (RCCL is)
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg)
     t.div_(dist.get_world_size(pg))
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
     return None
 
 
@@ -116,7 +124,7 @@ class GradBuckets:
         self.sync = True
         self.capture_log = None  # list: record bucket launches instead of issuing them
         self.launch_log = []     # bucket indices in launch order (tests / diagnostics)
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p, _, _ in layout]
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_acc) for p, _, _ in layout]
         self._hooks.append(F.register_grad_ready_hook(self._on_fused))
 
     def _add(self, entries, pad):
@@ -152,6 +160,13 @@ class GradBuckets:
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
+
+    def _on_acc(self, p):
+        # AccumulateGrad also runs (gradient-less) for parameters a fused unit sank in place:
+        # those are counted by the unit's own ready notification (_on_fused) only
+        if F.sunk_in_this_backward(p):
+            return
+        self._on_grad(p)
 
     def _on_fused(self, p):
         if p in self._bucket_of:

@@ -243,6 +243,7 @@ def _final_flush(task):
 
 def _defer_wgrad(p, g, dy2, x2):
     task = _task()
+    p._gvl_sunk_task = task
     if x2 is None:  # bias gradient
         _PENDING_B.append((task, p, g, dy2, torch.cuda.current_stream(dy2.device)))
     else:
@@ -306,8 +307,18 @@ def _sink(p, ctx=None):
 
 
 def _ready(p):
+    # The engine still runs p's AccumulateGrad node (and its post-accumulate-grad hooks)
+    # when the Function returned None for p; the mark tells gvl.dist.GradBuckets that this
+    # backward's gradient of p arrives through this path instead.
+    p._gvl_sunk_task = _task()
     for fn in _READY_HOOKS:
         fn(p)
+
+
+def sunk_in_this_backward(p):
+    """True when a fused unit accumulates p's gradient in place during the current backward
+    (its AccumulateGrad hook then carries no gradient)."""
+    return getattr(p, "_gvl_sunk_task", None) == _task()
 
 
 def _wgrad(ctx, i, p, dy2, x2, defer=False):

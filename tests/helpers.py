@@ -26,6 +26,20 @@ def recipe_params(keys_shapes, dtype=torch.float32, device="cpu"):
     return P
 
 
+def margins_out(name, rec):
+    """Write a parity test's measured errors as JSON under $GVL_MARGINS_DIR (default
+    gpurun_out/parity_margins; the GPU session copies them into profiles/)."""
+    import json
+    import os
+    d = os.environ.get("GVL_MARGINS_DIR", os.path.join("gpurun_out", "parity_margins"))
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{name}.json"), "w") as f:
+            json.dump(rec, f, indent=1, default=float)
+    except OSError:
+        pass
+
+
 def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

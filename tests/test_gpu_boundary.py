@@ -166,6 +166,12 @@ def test_default_vocab_50257(cuda):
 
 
 def test_out_of_range_ids_raise(cuda):
+    """Synchronous checks (the first gvl.functional.SYNC_CHECKS calls of a process) raise at
+    the op, like nn.Embedding / F.cross_entropy; later ones are asynchronous and raise on a
+    following call once the device verdict has landed (no host sync per micro-step)."""
+    from gvl import functional as Fn
+    Fn._ID_CHECKS[0] = 0
+    Fn._ID_INFLIGHT.clear()
     model, _ = _tiny_gpt(cuda)
     x, y = _batches(cuda, 1)[0]
     bad = x.clone()
@@ -184,6 +190,15 @@ def test_out_of_range_ids_raise(cuda):
     yign[0, :5] = -100  # ignore_index stays legal
     _, loss = model(x, yign)
     assert torch.isfinite(loss)
+    # asynchronous mode: the bad id does not stall the op; it raises on a later call
+    Fn._ID_CHECKS[0] = Fn.SYNC_CHECKS
+    with pytest.raises(IndexError, match="asynchronously"):
+        model(bad, y)  # (may already raise here: the target check polls the id verdict)
+        torch.cuda.synchronize()
+        model(x, y)
+    model(x, y)  # the verdict queue is clear again
+    torch.cuda.synchronize()
+    Fn._poll_id_checks()
 
 
 def test_checkpoint_manager_resume_with_arenas(cuda, tmp_path):
@@ -319,8 +334,12 @@ def test_deferred_wgrad_survives_failed_backward(cuda):
 
     class Boom(RuntimeError):
         pass
-    h = m.transformer.h[0].register_forward_hook(
-        lambda mod, a, out: out.register_hook(lambda g: (_ for _ in ()).throw(Boom())))
+    def boom(g):
+        raise Boom()
+
+    def hook(mod, a, out):
+        out.register_hook(boom)
+    h = m.transformer.h[0].register_forward_hook(hook)
     _, loss = m(*mbs[0])
     with pytest.raises(Boom):
         loss.backward()

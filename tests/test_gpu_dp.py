@@ -131,8 +131,9 @@ def test_overlap_eager_buckets_fire_during_backward(cuda):
 @pytest.mark.parametrize("kind", ["lm", "qformer"])
 def test_segmented_graph_step_matches_eager(cuda, kind):
     """The captured DP step (segment graphs + buckets issued between replays), world size 1
-    over RCCL: the buckets are logged into the segments that finalise them, and losses and
-    parameters track the eager bucketed train_step over 3 optimizer steps."""
+    over RCCL: the buckets are logged into the segments that finalise them, and the replayed
+    step's loss and gradients equal the eager bucketed train_step's on the same weights (the
+    tied wte's two contributions are summed in another order: close, not bitwise)."""
     from gvl.dist import GradBuckets
     from gvl.graph import GraphedStep
     from gvl.train import train_step
@@ -148,7 +149,7 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         ropt = ref.configure_optimizers(0.1, 1e-3, "cuda")
         rb = GradBuckets(ropt, bucket_mb=0.05, model=ref, force=True)
         losses_ref = [train_step(ref, ropt, mbs, loss_fn, 1e-3, buckets=rb).loss.item()
-                      for _ in range(5)]
+                      for _ in range(3)]
         m = build()
         opt = m.configure_optimizers(0.1, 1e-3, "cuda")
         b = GradBuckets(opt, bucket_mb=0.05, model=m, force=True)
@@ -158,13 +159,20 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         logged = [len(x) for x in gs.logs]
         print("buckets per segment", logged, "of", len(b.buckets))
         assert logged[0] >= 1 and sum(logged) == len(b.buckets)
-        losses = [gs(1e-3).loss.item() for _ in range(3)]
-        print("eager", losses_ref, "graphed", losses)
-        assert losses == pytest.approx(losses_ref[2:], rel=2e-3)
+        loss = gs(1e-3).loss.item()
+        torch.cuda.synchronize()
+        print("eager", losses_ref, "graphed step 3", loss)
+        assert loss == pytest.approx(losses_ref[2], rel=1e-6)
         for (n, p), q in zip(ref.named_parameters(), m.parameters()):
-            if p.requires_grad:
-                e = float((p.float() - q.float()).norm() / p.float().norm().clamp_min(1e-30))
-                assert e < 2e-2, (n, e)
+            if not p.requires_grad:
+                continue
+            if "wte" in n or "lm_head" in n:
+                e = float((p.grad.float() - q.grad.float()).norm() / p.grad.float().norm())
+                assert e < 1e-2, (n, e)
+            else:
+                assert torch.equal(p.grad, q.grad), n
+            e = float((p.float() - q.float()).norm() / p.float().norm().clamp_min(1e-30))
+            assert e < 1e-3, (n, e)
         rb.remove()
         b.remove()
     finally:
@@ -195,11 +203,11 @@ def _rank_main(rank, world, port, kind, graphed, q):
             gs = GraphedStep(m, opt, mbs, loss_fn, 1e-3, warmup=1, buckets=bk, cuts=cuts)
             res = gs(1e-3)
         else:
-            train_step(m, opt, mbs, loss_fn, 1e-3, buckets=bk)
             res = train_step(m, opt, mbs, loss_fn, 1e-3, buckets=bk)
         torch.cuda.synchronize()
+        # the step's all-reduced pre-clip gradients stay in the grad arena after the step
         q.put((rank, float(res.loss), float(res.norm),
-               {n: p.detach().float().cpu().numpy() for n, p in m.named_parameters()
+               {n: p.grad.detach().float().cpu().numpy() for n, p in m.named_parameters()
                 if p.requires_grad}))
         dist.destroy_process_group()
     except BaseException as e:
@@ -210,9 +218,13 @@ def _rank_main(rank, world, port, kind, graphed, q):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("kind,graphed", [("lm", False), ("lm", True), ("qformer", True)])
 def test_two_ranks_gloo_match_single_process(cuda, kind, graphed):
-    """2 ranks (both on cuda:0, gloo) x 2 micro-steps of gvl modules + gvl AdamW after two
-    optimizer steps (eager) / warm-up + one replay (graphed DP step) == one process over the
-    4 micro-batches: CFG3's accumulate-then-all-reduce and CFG5's bridge-only exchange."""
+    """2 ranks (both on cuda:0, gloo) x 2 micro-steps of gvl modules + gvl AdamW == one process
+    over the 4 micro-batches: CFG3's accumulate-then-all-reduce and CFG5's bridge-only
+    exchange.  Eager: one optimizer step; graphed DP step: an eager warm-up step + one replay.
+    Compared: loss, grad norm and every all-reduced gradient (identical on both ranks; vs the
+    single process within bf16 summation-order noise).  Parameters after the AdamW update are
+    not compared element-wise: Adam normalises every element, so a gradient that differs by
+    rounding noise moves a near-zero-gradient weight by up to lr in either direction."""
     from gvl.graph import GraphedStep
     from gvl.train import train_step
     ctx = mp.get_context("spawn")
@@ -239,16 +251,15 @@ def test_two_ranks_gloo_match_single_process(cuda, kind, graphed):
     if graphed:
         res = GraphedStep(m, opt, mbs, loss_fn, 1e-3, warmup=1)(1e-3)
     else:
-        train_step(m, opt, mbs, loss_fn, 1e-3)
         res = train_step(m, opt, mbs, loss_fn, 1e-3)
     print(f"{kind} graphed={graphed}: DP loss {l0:.6f} single {res.loss.item():.6f}; norm "
           f"{n0:.5f} vs {res.norm.item():.5f}")
     assert l0 == pytest.approx(res.loss.item(), rel=2e-3)
     assert n0 == pytest.approx(res.norm.item(), rel=3e-2)
-    worst = 0.0
+    worst = (0.0, "")
     for n, p in m.named_parameters():
         if p.requires_grad:
-            a = p.detach().float().cpu().numpy()
-            worst = max(worst, float(np.linalg.norm(a - p0[n]) / max(np.linalg.norm(a), 1e-30)))
-    print("worst param rel-L2", worst)
-    assert worst < 2e-2
+            a = p.grad.detach().float().cpu().numpy()
+            worst = max(worst, (float(np.linalg.norm(a - p0[n]) / max(np.linalg.norm(a), 1e-30)), n))
+    print("worst gradient rel-L2 vs the single process", worst)
+    assert worst[0] < (2e-2 if graphed else 1e-2), worst
