@@ -159,15 +159,28 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
   }
   const int nkt = (int)((kend + KT - 1) / KT);
 
-  float4_t o[G][4];
+#ifndef GVL_ATTN_FWD_V2
+#define GVL_ATTN_FWD_V2 1
+#endif
+#if GVL_ATTN_FWD_V2
+  // o[g][4] = row sum of the bf16 P (an MFMA against a ones fragment: the softmax
+  // denominator of exactly the P values that enter P.V, and 16 fewer VALU adds per tile)
+  constexpr int NO = 5;
+#else
+  constexpr int NO = 4;
+#endif
+  float4_t o[G][NO];
   float m[G], l[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NO; ++t) o[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
     m[g] = -INFINITY;
     l[g] = 0.f;
   }
+  short8_t ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
 
   uint4 rk[2], rv[2];
   load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
@@ -213,25 +226,48 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
             if (kk >= kl || (p.causal && kk > ql)) sc[g][n][r] = -INFINITY;
           }
       }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[g][n][r]);
+      float mx = fmaxf(fmaxf(sc[g][0][0], sc[g][0][1]), sc[g][0][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][0][3]), sc[g][1][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][1][1]), sc[g][1][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][1][3]), sc[g][2][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][2][1]), sc[g][2][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][2][3]), sc[g][3][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][3][1]), sc[g][3][2]);
+      mx = fmaxf(mx, sc[g][3][3]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+#if GVL_ATTN_FWD_V2
+      // deferred rescale (T13): keep the running max while no row's max grew by more than
+      // RESCALE_LOG2 (P then stays <= 2^4 before normalisation); rescale O and the row sum
+      // only when some row of the wave needs it — every P of this tile is exponentiated
+      // against the max the decision leaves, after the previous tile's P.V completed
+      constexpr float RESCALE_LOG2 = 4.f;
+      const float cand = mx * p.c2;
+      if (!__all(cand - m[g] <= RESCALE_LOG2)) {
+        const float mnew = fmaxf(m[g], cand);
+        const float msub0 = (mnew == -INFINITY) ? 0.f : mnew;
+        const float alpha = __builtin_amdgcn_exp2f(m[g] - msub0);
+        m[g] = mnew;
+#pragma unroll
+        for (int t = 0; t < NO; ++t) o[g][t] *= alpha;
+        l[g] *= alpha;
+      }
+      const float msub = (m[g] == -INFINITY) ? 0.f : m[g];
+      float ls = 0.f;  // (dropout: the denominator counts the un-dropped probabilities)
+#else
       const float mnew = fmaxf(m[g], mx * p.c2);
       const float msub = (mnew == -INFINITY) ? 0.f : mnew;
       const float alpha = __builtin_amdgcn_exp2f(m[g] - msub);
       m[g] = mnew;
       float ls = 0.f;
+#endif
       const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q[g]) * (uint64_t)p.Tk;
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -msub));
-          ls += e;
+          if (!GVL_ATTN_FWD_V2 || DROP) ls += e;
           float pe = e;
           if constexpr (DROP) {
             const int64_t key = k0 + 16 * n + 4 * Gl + r;
@@ -239,11 +275,16 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
           }
           sc[g][n][r] = pe;
         }
+#if !GVL_ATTN_FWD_V2
       l[g] = l[g] * alpha + ls;
 #pragma unroll
       for (int t = 0; t < 4; ++t) o[g][t] *= alpha;
+#endif
       pf[g][0] = pack_frag(sc[g][0], sc[g][1]);
       pf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+#if GVL_ATTN_FWD_V2
+      if constexpr (DROP) l[g] += ls;
+#endif
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -253,6 +294,12 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
 #pragma unroll
         for (int g = 0; g < G; ++g) o[g][t] = mfma16(vf, pf[g][s], o[g][t]);
       }
+#if GVL_ATTN_FWD_V2
+      if constexpr (!DROP) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) o[g][4] = mfma16(ones, pf[g][s], o[g][4]);
+      }
+#endif
     }
     if (more) {
       store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
@@ -265,6 +312,9 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
     float lt = l[g];
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
+#if GVL_ATTN_FWD_V2
+    if constexpr (!DROP) lt = o[g][4][0];
+#endif
     if (!qok[g]) continue;
     const float inv = 1.f / lt;
     bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q[g] * p.o_st;
@@ -276,6 +326,7 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
     }
     if (Gl == 0 && p.lse) p.lse[(b * p.H + h) * p.Tq + q[g]] = (m[g] + log2f(lt)) * LN2;
   }
+  (void)l;
 }
 
 // ------------------------------------------------------------------------------------

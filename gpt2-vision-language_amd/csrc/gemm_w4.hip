@@ -230,6 +230,97 @@ __device__ __forceinline__ void gemm_w4_body(const GemmP& p) {
 #pragma unroll
   for (int i = 0; i < FM; ++i) af[i] = SA::frag(smem, arow + 16 * i, lane);
 
+#ifndef GVL_W4_ORDER
+#define GVL_W4_ORDER 0
+#endif
+#if GVL_W4_ORDER == 3
+// Variant: the step is cut into MFMA chunks pinned in source order by sched_barrier(0), with
+// the step's memory operations placed between them by hand: the LDS writes of step C+2 lead
+// (chunk 0), the global reloads of that register set follow, and the fragment reads of step
+// C+1 are spread over the remaining chunks, so every MFMA gap carries at most a few issues.
+#define W4_SB() __builtin_amdgcn_sched_barrier(0)
+#define GVL_W4_STEP(C, SET, CA, CB, NA, NB)                                                 \
+  do {                                                                                      \
+    const char* sl_ = smem + (((SET) + 2) % 3) * SLOT; /* step C+1's slot */                \
+    static_assert(FN == 4, "chunking assumes 4 B fragments");                                \
+    /* chunk 0: writes of step C+2 + MFMA row 0 */                                          \
+    W4_DIAG_MEM(GVL_W4_WRITE((C) + 2, SET));                                                \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[0][j] = mfma16(CB[j], CA[0], acc[0][j]); \
+    W4_SB();                                                                                \
+    W4_DIAG_MEM(GVL_W4_LOAD(SET));                                                          \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[1][j] = mfma16(CB[j], CA[1], acc[1][j]); \
+    W4_SB();                                                                                \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                           \
+        NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                             \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[2][j] = mfma16(CB[j], CA[2], acc[2][j]); \
+    W4_SB();                                                                                \
+    _Pragma("unroll") for (int j = 2; j < 4; ++j)                                           \
+        NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                             \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[3][j] = mfma16(CB[j], CA[3], acc[3][j]); \
+    W4_SB();                                                                                \
+    _Pragma("unroll") for (int i = 0; i < FM / 2; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
+    _Pragma("unroll") for (int i = 4; i < FM; ++i)                                          \
+        _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]); \
+    W4_SB();                                                                                \
+    _Pragma("unroll") for (int i = FM / 2; i < FM; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
+    W4_DIAG_BAR();                                                                          \
+  } while (0)
+#elif GVL_W4_ORDER == 2
+// Variant: the LDS writes of step C+2 are pinned at the head of the step (sched_barrier), the
+// register set is reloaded after them (no AGPR parking of the staged data), and the step's
+// fragment reads and global loads are spread between its MFMAs.
+constexpr int W4_NR = FM + (BMN ? 2 * FN : FN);  // DS reads per step (tr reads: 2 per B frag)
+#define W4_INTERLEAVE2()                                                          \
+  do {                                                                            \
+    _Pragma("unroll") for (int q_ = 0; q_ < W4_NR; ++q_) {                        \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
+    }                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < PA + PB; ++q_) {                      \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                          \
+    }                                                                             \
+    if constexpr (FM * FN > W4_NR + PA + PB)                                      \
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN - W4_NR - PA - PB, 0);  \
+  } while (0)
+#define GVL_W4_STEP(C, SET, CA, CB, NA, NB)                                                 \
+  do {                                                                                      \
+    W4_DIAG_MEM(GVL_W4_WRITE((C) + 2, SET));                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    { /* step C+1 in slot (SET + 2) % 3 */                                                  \
+      const char* sl_ = smem + (((SET) + 2) % 3) * SLOT;                                    \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
+          NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                           \
+      _Pragma("unroll") for (int i = 0; i < FM; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
+    }                                                                                       \
+    W4_DIAG_MEM(GVL_W4_LOAD(SET));                                                          \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                          \
+        _Pragma("unroll") for (int j = 0; j < FN; ++j)                                      \
+            acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]);                                    \
+    W4_INTERLEAVE2();                                                                       \
+    W4_DIAG_BAR();                                                                          \
+  } while (0)
+#elif GVL_W4_ORDER == 1
+// Variant: the LDS writes of step C+2 lead the step (right after the barrier that retired
+// slot (C+2)%3's reads), so their VGPR->LDS transfer overlaps the MFMAs instead of queueing
+// behind them before the barrier; the register set is reloaded after the fragment reads.
+#define GVL_W4_STEP(C, SET, CA, CB, NA, NB)                                                 \
+  do {                                                                                      \
+    W4_DIAG_MEM(GVL_W4_WRITE((C) + 2, SET));                                                \
+    { /* step C+1 in slot (SET + 2) % 3 */                                                  \
+      const char* sl_ = smem + (((SET) + 2) % 3) * SLOT;                                    \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
+          NB[j] = SB::frag(sl_ + SA::BYTES, bcol + 16 * j, lane);                           \
+      _Pragma("unroll") for (int i = 0; i < FM; ++i) NA[i] = SA::frag(sl_, arow + 16 * i, lane); \
+    }                                                                                       \
+    W4_DIAG_MEM(GVL_W4_LOAD(SET));                                                          \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                          \
+        _Pragma("unroll") for (int j = 0; j < FN; ++j)                                      \
+            acc[i][j] = mfma16(CB[j], CA[i], acc[i][j]);                                    \
+    W4_INTERLEAVE();                                                                        \
+    W4_DIAG_BAR();                                                                          \
+  } while (0)
+#else
 #define GVL_W4_STEP(C, SET, CA, CB, NA, NB)                                                 \
   do {                                                                                      \
     { /* step C+1 in slot (SET + 2) % 3 */                                                  \
@@ -247,6 +338,7 @@ __device__ __forceinline__ void gemm_w4_body(const GemmP& p) {
     W4_INTERLEAVE();                                                                        \
     W4_DIAG_BAR();                                                                          \
   } while (0)
+#endif
 
   int c = 0;
   for (int t = 0; t < ntl; ++t) {

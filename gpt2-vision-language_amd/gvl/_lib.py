@@ -90,6 +90,8 @@ SIGNATURES = {
                                     c_i64, c_vp]),
     "gvl_embedding_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64,
                                     c_i64, c_vp]),
+    "gvl_copy_rows": (C.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64,
+                                c_i64, c_i64, c_i32, c_vp]),
     "gvl_embedding_bwd_workspace": (c_i64, [c_i64]),
     "gvl_embedding_bwd_det": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                         c_i64, c_i64, c_vp, c_i64, c_vp]),

@@ -137,7 +137,7 @@ class BLIP2Bridge(nn.Module):
     def forward(self, patch_tokens):
         x = Fn.LinearFn.apply(patch_tokens, bf(self.vis_proj.weight), bf(self.vis_proj.bias))
         B = x.shape[0]
-        q = bf(self.query_tokens).unsqueeze(0).expand(B, -1, -1)
+        q = Fn.QueryExpandFn.apply(self.query_tokens, B)  # query_tokens.expand(B, -1, -1)
         for layer in self.layers:
             q = layer(q, x)
         return q

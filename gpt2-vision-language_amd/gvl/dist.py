@@ -35,6 +35,14 @@ from . import functional as F
 
 # GPT-2 blocks per in-backward flush of the deferred weight gradients on the sync micro-step
 OVERLAP_BLOCKS = int(os.environ.get("GVL_DP_OVERLAP_BLOCKS", "4"))
+# GVL_TRACE_BUCKETS=1: a roctx marker per bucket issue (rocprofv3 --marker-trace shows where
+# each all-reduce enters the stream relative to the backward kernels)
+TRACE = os.environ.get("GVL_TRACE_BUCKETS") == "1"
+
+
+def _mark(name):
+    if TRACE:
+        torch.cuda.nvtx.mark(name)
 
 
 def _is_nccl(pg):
@@ -137,6 +145,7 @@ class GradBuckets:
             self.capture_log.append(bi)
             return
         self.launch_log.append(bi)
+        _mark(f"gvl.bucket{bi}")
         for s, e in self.buckets[bi][0]:
             h = _avg(self.opt.grad_arena[s:e], self.pg, async_op=True)
             if h is not None:
@@ -146,6 +155,7 @@ class GradBuckets:
         """Issue the all-reduces of buckets recorded during a capture (gvl.graph replay)."""
         for bi in indices:
             self.launch_log.append(bi)
+            _mark(f"gvl.bucket{bi}")
             for s, e in self.buckets[bi][0]:
                 h = _avg(self.opt.grad_arena[s:e], self.pg, async_op=True)
                 if h is not None:

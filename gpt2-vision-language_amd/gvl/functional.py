@@ -865,8 +865,10 @@ class EmbedFn(torch.autograd.Function):
         M = 0 if prefix is None else prefix.shape[1]
         S = M + T
         out = torch.empty(B, S, C, dtype=BF16, device=idx.device)
-        if prefix is not None:
-            out[:, :M].copy_(prefix)
+        if prefix is not None:  # the image tokens in front (torch.cat, model.py:191)
+            pre = prefix if prefix.dtype == BF16 else prefix.to(BF16)
+            pre = pre.contiguous()
+            K.copy_rows(pre.view(B * M, C), out.view(B * S, C), M, B, M, 0, S, 0)
         K.embedding_fwd(idx, wte, wpe, out, T, S, M)
         if any(ctx.needs_input_grad):  # (grad mode is off inside forward)
             ctx.save_for_backward(idx)
@@ -950,9 +952,9 @@ class LMHeadLossFn(torch.autograd.Function):
             dxt = K.gemm(dl, w, b_mn=True, alpha_ptr=scale)
             if off == 0 and T == S:
                 dx = dxt.view(B, S, C)
-            else:
-                dx = torch.zeros(B, S, C, dtype=BF16, device=dl.device)
-                dx[:, off:off + T] = dxt.view(B, T, C)
+            else:  # text rows at their offset, the image rows' gradient is zero
+                dx = torch.empty(B, S, C, dtype=BF16, device=dl.device)
+                K.copy_rows(dxt, dx.view(B * S, C), T, B, T, 0, S, off, zero_rest=True)
         if ctx.needs_input_grad[1]:
             if off == 0 and T == S:
                 xt = x2
@@ -965,6 +967,37 @@ class LMHeadLossFn(torch.autograd.Function):
             else:
                 dw = K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale)
         return dx, dw, None, None, None, None, None
+
+
+class QueryExpandFn(torch.autograd.Function):
+    """query_tokens.unsqueeze(0).expand(B, -1, -1) materialised once as a contiguous [B, Q, C]
+    bf16 tensor (gpt2_q_former/model.py:160-161); backward: the batch sum as one column-sum
+    kernel over [B, Q*C] (into the arena gradient when it sinks) instead of ATen's reduce."""
+
+    @staticmethod
+    def forward(ctx, q, B: int):
+        Q, C = q.shape
+        qb = q if q.dtype == BF16 else q.to(BF16)
+        out = torch.empty(B, Q, C, dtype=BF16, device=q.device)
+        K.copy_rows(qb.contiguous(), out.view(B * Q, C), Q, B, 0, 0, Q, 0)
+        if ctx.needs_input_grad[0]:
+            ctx.params = (q,)
+            ctx.shape = (B, Q, C, q.dtype)
+            _mark(ctx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, Q, C, dt = ctx.shape
+        d2 = dout.to(BF16).contiguous().view(B, Q * C)
+        p = ctx.params[0]
+        g = _sink(p, ctx)
+        if g is not None:
+            K.colsum(d2, out=g.view(-1), accumulate=True)
+            _ready(p)
+            return None, None
+        dq = K.colsum(d2).view(Q, C)
+        return (dq if dt == BF16 else dq.to(dt)), None
 
 
 def lm_head_loss(x, w, targets, row_offset=0, mask=None, mask_mode=False):

@@ -434,6 +434,19 @@ def embedding_bwd(idx, dout, dwte_acc, dwpe_acc, T, out_rows_per_seq, out_offset
                                       out_offset, _stream()), "gvl_embedding_bwd")
 
 
+def copy_rows(src, dst, T, G, src_rows, src_off, dst_rows, dst_off, zero_rest=False):
+    """Grouped row copy (gvl_copy_rows) between row-major bf16 2-D views: dst row
+    (g*dst_rows + dst_off + t) = src row (g*src_rows + src_off + t); zero_rest zeroes the
+    other rows of every dst group.  src_rows = 0 broadcasts T rows to all G groups."""
+    _dev(src, dst)
+    if src.dtype != BF16 or dst.dtype != BF16 or src.stride(-1) != 1 or dst.stride(-1) != 1:
+        raise TypeError("gvl.copy_rows: bf16 row-major views expected")
+    _lib.check(_L().gvl_copy_rows(src.data_ptr(), src.stride(0), src_rows, src_off,
+                                  dst.data_ptr(), dst.stride(0), dst_rows, dst_off, T, G,
+                                  dst.shape[-1], int(zero_rest), _stream()), "gvl_copy_rows")
+    return dst
+
+
 _EMB_KEYS = {}
 
 

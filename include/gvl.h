@@ -226,6 +226,15 @@ int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dwte_acc, flo
  * both accumulate into one arena gradient.  `keys`: uint32 scratch of
  * gvl_embedding_bwd_workspace(n_tokens) entries.  C % 8 == 0, C <= 1024, vocab < 2^18 - 1,
  * n_tokens % T == 0; ids outside [0, vocab) contribute nothing. */
+/* ABI v6: grouped bf16 row copy: for g < G and t < T, dst row (g*dst_rows + dst_off + t) =
+ * src row (g*src_rows + src_off + t) (src_rows = 0 broadcasts one block of T rows to every
+ * group); with zero_rest the other dst_rows - T rows of each group are zeroed.  Replaces the
+ * caption path's torch.cat of image tokens before the text embeddings
+ * (gpt2_linear/model.py:191), query_tokens.expand (gpt2_q_former/model.py:160-161) and the
+ * zero-filled [B, S, C] gradient around the text-row lm_head gradient (model.py:219-230). */
+int gvl_copy_rows(const void* src, int64_t ld_src, int64_t src_rows, int64_t src_off, void* dst,
+                  int64_t ld_dst, int64_t dst_rows, int64_t dst_off, int64_t T, int64_t G,
+                  int64_t cols, int32_t zero_rest, gvl_stream_t stream);
 int64_t gvl_embedding_bwd_workspace(int64_t n_tokens);
 int gvl_embedding_bwd_det(const int64_t* idx, const void* dout, void* dwte, void* dwpe,
                           int64_t n_tokens, int64_t T, int64_t C, int64_t vocab,
