@@ -128,7 +128,7 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 // Short sequences (G = 1, no dropout) compile for 4 waves per SIMD (<= 128 VGPRs, no spill):
 // 4 blocks per CU instead of 3, so the caption decoder's 1536 (b, h) blocks take 1.5 rounds.
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel(AttnP p) {
+__global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
@@ -1189,6 +1189,17 @@ int pick_groups(int64_t T) {
   return T > 64 ? 2 : 1;
 }
 
+// Forward query groups per wave: GVL_ATTN_FWD_G=4 runs 64 query rows per wave (one wave per
+// SIMD: K/V fragments read from LDS once per 64 rows instead of 32) when Tq > 128, no dropout.
+int pick_fwd_groups(int64_t T, bool drop) {
+  static const int g4 = [] {
+    const char* e = getenv("GVL_ATTN_FWD_G");
+    return e ? atoi(e) : 0;
+  }();
+  if (g4 == 4 && T > 128 && !drop) return 4;
+  return pick_groups(T);
+}
+
 // dK/dV key groups per wave: GVL_DKDV_G=2 runs 32 keys per wave (one wave per SIMD, the
 // accumulators need > 256 registers) for Tk > 64; default 1.
 int dkdv_groups(int64_t Tk) {
@@ -1235,10 +1246,12 @@ unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntil
 extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   AttnP p;
   if (fill(d, p)) return -1;
-  const int G = pick_groups(d->Tq);
+  const int G = pick_fwd_groups(d->Tq, p.has_drop != 0);
   dim3 grid(grid_1d(d, (d->Tq + 64 * G - 1) / (64 * G)));
   hipStream_t s = gvl::as_stream(stream);
-  if (G == 2) {
+  if (G == 4) {
+    gvl::launch_timed(attn_fwd_kernel<4, false>, grid, dim3(NT), 0, s, p);
+  } else if (G == 2) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
   } else {

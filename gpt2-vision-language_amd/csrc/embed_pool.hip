@@ -60,40 +60,69 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int64_t* __restrict_
 // ---- deterministic embedding backward (ABI v6) -------------------------------------------
 // dwte[v] += sum of dout rows of the tokens with id v, in token order, one fp32 sum per row
 // and ONE bf16 read-modify-write per touched row (no atomics: bit-identical run to run).
-// A chunk of <= EMB_CHUNK tokens is sorted by key (id << 14 | position) with a bitonic sort
-// in LDS by one 1024-thread block; then one wave per sorted slot: the head of each run of
-// equal ids sums its run and updates the row.  Larger inputs run chunk after chunk (the
-// launches are stream-ordered, so a row touched by two chunks is updated in chunk order).
-constexpr int EMB_CHUNK = 16384;  // 64 KiB of keys in LDS
-constexpr uint32_t EMB_BAD = 0xFFFFFFFFu;
+// A chunk of <= EMB_CHUNK tokens is sorted by the unique key (id << 14 | position) in two
+// launches: every 1024-key tile is bitonic-sorted in LDS by its own block (emb_tile_kernel),
+// then each key's global rank = its index in its tile + the number of smaller keys in every
+// other tile (binary searches in LDS, emb_rank_kernel) scatters it to its sorted slot.  Then
+// one wave per sorted slot: the head of each run of equal ids sums its run and updates the
+// row.  Larger inputs run chunk after chunk (stream-ordered, so a row touched by two chunks
+// is updated in chunk order).  Out-of-range ids get the reserved id field EMB_BAD_ID (still
+// unique keys: the position is kept) and are skipped.
+constexpr int EMB_CHUNK = 16384;  // 14-bit positions
+constexpr int EMB_TILE = 1024;
+constexpr uint32_t EMB_BAD_ID = 0x3FFFFu;
 constexpr int EMB_MAXC = 1024;    // 64 lanes x 8 bf16 x 2 slices
 
-__global__ __launch_bounds__(1024) void emb_sort_kernel(const int64_t* __restrict__ idx,
-                                                        int64_t base, int n, int npow,
-                                                        int64_t V, uint32_t* __restrict__ out) {
-  __shared__ uint32_t s[EMB_CHUNK];
-  for (int i = threadIdx.x; i < npow; i += 1024) {
-    uint32_t key = EMB_BAD;
-    if (i < n) {
-      const int64_t id = idx[base + i];
-      if (id >= 0 && id < V) key = ((uint32_t)id << 14) | (uint32_t)i;
+__global__ __launch_bounds__(EMB_TILE / 2) void emb_tile_kernel(const int64_t* __restrict__ idx,
+                                                                int64_t base, int n, int64_t V,
+                                                                uint32_t* __restrict__ tiles) {
+  __shared__ uint32_t s[EMB_TILE];
+  const int t0 = blockIdx.x * EMB_TILE;
+  for (int i = threadIdx.x; i < EMB_TILE; i += EMB_TILE / 2) {
+    const int p = t0 + i;
+    uint32_t key = 0xFFFFFFFFu;  // pad: >= every real key, never ranked below n
+    if (p < n) {
+      const int64_t id = idx[base + p];
+      key = ((id >= 0 && id < V) ? (uint32_t)id : EMB_BAD_ID) << 14 | (uint32_t)p;
     }
     s[i] = key;
   }
   __syncthreads();
-  for (int k = 2; k <= npow; k <<= 1) {
+  const int t = threadIdx.x;
+  for (int k = 2; k <= EMB_TILE; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < (npow >> 1); t += 1024) {
-        const int i = 2 * j * (t / j) + (t % j);
-        const int l = i + j;
-        const uint32_t a = s[i], b = s[l];
-        const bool up = (i & k) == 0;
-        if ((a > b) == up) { s[i] = b; s[l] = a; }
-      }
+      const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+      const int l = i + j;
+      const uint32_t a = s[i], b = s[l];
+      const bool up = (i & k) == 0;
+      if ((a > b) == up) { s[i] = b; s[l] = a; }
       __syncthreads();
     }
   }
-  for (int i = threadIdx.x; i < n; i += 1024) out[i] = s[i];
+  for (int i = threadIdx.x; i < EMB_TILE; i += EMB_TILE / 2) tiles[t0 + i] = s[i];
+}
+
+// lower_bound: number of entries of the sorted tile p[0, EMB_TILE) that are < key
+GVL_DEV int emb_count_less(const uint32_t* p, uint32_t key) {
+  int lo = 0;
+#pragma unroll
+  for (int step = EMB_TILE / 2; step > 0; step >>= 1)
+    if (p[lo + step - 1] < key) lo += step;
+  return lo + (p[lo] < key ? 1 : 0);
+}
+
+__global__ __launch_bounds__(EMB_TILE) void emb_rank_kernel(const uint32_t* __restrict__ tiles,
+                                                            int ntiles, int n,
+                                                            uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t all[];
+  for (int i = threadIdx.x; i < ntiles * EMB_TILE; i += EMB_TILE) all[i] = tiles[i];
+  __syncthreads();
+  const int me = blockIdx.x;
+  const uint32_t key = all[me * EMB_TILE + threadIdx.x];
+  int rank = threadIdx.x;
+  for (int u = 0; u < ntiles; ++u)
+    if (u != me) rank += emb_count_less(all + u * EMB_TILE, key);
+  if (rank < n) out[rank] = key;
 }
 
 __global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict__ keys, int n,
@@ -103,8 +132,8 @@ __global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const uint32_t key = keys[i];
-  if (key == EMB_BAD) return;
   const uint32_t id = key >> 14;
+  if (id == EMB_BAD_ID) return;
   if (i > 0 && (keys[i - 1] >> 14) == id) return;  // not the head of its run
   const int lane = threadIdx.x & 63;
   float acc[2][8];
@@ -114,7 +143,7 @@ __global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict
     for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
   for (int j = i; j < n; ++j) {
     const uint32_t kj = keys[j];
-    if ((kj >> 14) != id || kj == EMB_BAD) break;
+    if ((kj >> 14) != id) break;
     const int64_t r = base + (int64_t)(kj & 0x3FFFu);
     const bf16_t* g = dout + ((r / T) * S + off + r % T) * (int64_t)C;
 #pragma unroll
@@ -156,16 +185,26 @@ __global__ __launch_bounds__(256) void emb_pos_kernel(const bf16_t* __restrict__
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
-  for (int64_t g = 0; g < G; ++g) {
-    const bf16_t* src = dout + (g * S + off + t) * (int64_t)C;
+  // four rows' loads in flight, then summed in sequence order (fixed order: deterministic)
+  for (int64_t g0 = 0; g0 < G; g0 += 4) {
+    uint4 u[4][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = lane * 8 + h * 512;
-      if (c < C) {
-        const uint4 u = *reinterpret_cast<const uint4*>(src + c);
-        acc[h][0] += lo_bf(u.x); acc[h][1] += hi_bf(u.x); acc[h][2] += lo_bf(u.y);
-        acc[h][3] += hi_bf(u.y); acc[h][4] += lo_bf(u.z); acc[h][5] += hi_bf(u.z);
-        acc[h][6] += lo_bf(u.w); acc[h][7] += hi_bf(u.w);
+    for (int q = 0; q < 4; ++q) {
+      const bf16_t* src = dout + ((g0 + q < G ? g0 + q : g0) * S + off + t) * (int64_t)C;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane * 8 + h * 512;
+        u[q][h] = c < C ? *reinterpret_cast<const uint4*>(src + c) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (g0 + q >= G) break;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[h][0] += lo_bf(u[q][h].x); acc[h][1] += hi_bf(u[q][h].x); acc[h][2] += lo_bf(u[q][h].y);
+        acc[h][3] += hi_bf(u[q][h].y); acc[h][4] += lo_bf(u[q][h].z); acc[h][5] += hi_bf(u[q][h].z);
+        acc[h][6] += lo_bf(u[q][h].w); acc[h][7] += hi_bf(u[q][h].w);
       }
     }
   }
@@ -304,7 +343,9 @@ extern "C" int gvl_embedding_bwd(const int64_t* idx, const void* dout, float* dw
 }
 
 extern "C" int64_t gvl_embedding_bwd_workspace(int64_t n_tokens) {
-  return n_tokens < EMB_CHUNK ? n_tokens : EMB_CHUNK;
+  // sorted tiles (padded to whole tiles) + the merged keys of one chunk
+  const int64_t n = n_tokens < EMB_CHUNK ? n_tokens : EMB_CHUNK;
+  return (n + EMB_TILE - 1) / EMB_TILE * EMB_TILE + n;
 }
 
 extern "C" int gvl_embedding_bwd_det(const int64_t* idx, const void* dout, void* dwte, void* dwpe,
@@ -322,10 +363,12 @@ extern "C" int gvl_embedding_bwd_det(const int64_t* idx, const void* dout, void*
                 "gvl_embedding_bwd_det: key workspace too small");
     for (int64_t base = 0; base < n_tokens; base += EMB_CHUNK) {
       const int n = (int)((n_tokens - base) < EMB_CHUNK ? (n_tokens - base) : EMB_CHUNK);
-      int npow = 64;
-      while (npow < n) npow <<= 1;
-      hipLaunchKernelGGL(emb_sort_kernel, dim3(1), dim3(1024), 0, s, idx, base, n, npow, vocab,
-                         keys);
+      const int nt = (n + EMB_TILE - 1) / EMB_TILE;
+      uint32_t* tiles = keys + n;
+      hipLaunchKernelGGL(emb_tile_kernel, dim3(nt), dim3(EMB_TILE / 2), 0, s, idx, base, n, vocab,
+                         tiles);
+      hipLaunchKernelGGL(emb_rank_kernel, dim3(nt), dim3(EMB_TILE), nt * EMB_TILE * sizeof(uint32_t),
+                         s, (const uint32_t*)tiles, nt, n, keys);
       hipLaunchKernelGGL(emb_seg_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s,
                          (const uint32_t*)keys, n, base, static_cast<const bf16_t*>(dout),
                          static_cast<bf16_t*>(dwte), T, (int)C, out_rows_per_seq, out_offset);

@@ -695,7 +695,7 @@ def _attn_case(cuda, B, H, Tq, Tk, causal, packed, drop_p=0.0, seed=0, grad=True
         assert e < 2.5e-2, f"{nm} rel err {e}"
 
 
-@pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (3, 12, 63), (2, 3, 64), (1, 1, 7)])
+@pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (2, 2, 300), (3, 12, 63), (2, 3, 64), (1, 1, 7)])
 def test_attention_causal(cuda, B, H, T):
     _attn_case(cuda, B, H, T, T, True, packed=True)
 
@@ -781,6 +781,54 @@ def test_embedding_fwd_bwd(cuda):
     ((wr[idx] + pr[:T]) * dout[:, M:].float()).sum().backward()
     assert rel_err(ate.cpu().numpy(), wr.grad.numpy()) < 1e-5
     assert rel_err(ape.cpu().numpy(), pr.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["small", "lm", "hot", "chunks"])
+def test_embedding_bwd_det_bit_exact(cuda, case):
+    """gvl_embedding_bwd_det: per-id fp32 sums in token order, one bf16 update per row —
+    emulated exactly on the host (np.add.at applies its updates in index order), so the
+    result must match BIT FOR BIT, including hot ids (one id repeated thousands of times),
+    out-of-range ids (skipped), a token count that is not a whole number of sort tiles and
+    inputs longer than one 16,384-token chunk (chunks applied in order)."""
+    K_ = _k()
+    V, C, G, T, M = {"small": (300, 128, 3, 20, 4), "lm": (50304, 768, 16, 1024, 0),
+                     "hot": (1000, 256, 5, 700, 2), "chunks": (4000, 64, 9, 4000, 1)}[case]
+    gen = torch.Generator().manual_seed(11)
+    idx = torch.randint(0, V, (G, T), generator=gen)
+    if case == "hot":
+        idx[:, ::2] = 7          # 1,750 copies of id 7, interleaved
+        idx[1, 5] = V + 3        # out of range: contributes nothing
+        idx[2, 9] = -1
+    dout = torch.randn(G, M + T, C, generator=gen).to(BF)
+    w0 = torch.randn(V, C, generator=gen).to(BF)
+    p0 = torch.randn(T + 5, C, generator=gen).to(BF)
+    gte, gpe = w0.to(cuda), p0.to(cuda)
+    K_.embedding_bwd_det(idx.to(cuda), dout.to(cuda), gte, gpe, T, M + T, M, C, V)
+    # host emulation, chunk by chunk (16,384 tokens) and position by position within a chunk
+    ids = idx.reshape(-1).numpy()
+    rows = dout[:, M:].reshape(-1, C).float().numpy()
+    want = w0.clone()
+    for c0 in range(0, ids.size, 16384):
+        ci, cr = ids[c0:c0 + 16384], rows[c0:c0 + 16384]
+        ok = (ci >= 0) & (ci < V)
+        acc = np.zeros((V, C), np.float32)
+        np.add.at(acc, ci[ok], cr[ok])
+        touched = np.unique(ci[ok])
+        upd = want.float().numpy()
+        upd[touched] = upd[touched] + acc[touched]
+        want = torch.from_numpy(upd).to(BF)
+    assert torch.equal(gte.cpu().view(torch.int16), want.view(torch.int16)), case
+    pacc = dout[:, M:].float().numpy()
+    ps = np.zeros((T, C), np.float32)
+    for g in range(G):
+        ps += pacc[g]
+    wp = p0.float().numpy().copy()
+    wp[:T] += ps
+    assert torch.equal(gpe.cpu().view(torch.int16), torch.from_numpy(wp).to(BF).view(torch.int16))
+    # and run to run
+    again = w0.to(cuda)
+    K_.embedding_bwd_det(idx.to(cuda), dout.to(cuda), again, None, T, M + T, M, C, V)
+    assert torch.equal(again, gte)
 
 
 @pytest.mark.parametrize("side", [16, 14])
