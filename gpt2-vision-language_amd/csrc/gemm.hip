@@ -229,8 +229,12 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     } else if ((env().cfg < 0 || env().cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, env().cfg == 10)) {
       // (cfg 11: default routing with the four-wave kernel off)
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
-      snprintf(buf, len, "%s<3, %s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
-               tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
+      if (gvl::gemm_w4d_ok(p))
+        snprintf(buf, len, "%s<%s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4dm_kernel" : "gemm_w4d_kernel",
+                 tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
+      else
+        snprintf(buf, len, "%s<3, %s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
+                 tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
     } else if (env().cfg >= 0 && env().cfg != 11) {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg == 10 ? 3 : env().cfg),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);

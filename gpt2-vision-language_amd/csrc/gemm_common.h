@@ -500,4 +500,6 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_rows128(const GemmP& p);  // the launch uses 128-row tiles (gemm_w4m_kernel)
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
+bool gemm_w4d_ok(const GemmP& p);  // gemm_w4d.hip: direct-A variant for a w4-planned shape
+int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s);
 }  // namespace gvl

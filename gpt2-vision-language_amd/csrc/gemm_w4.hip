@@ -488,6 +488,11 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
 bool gemm_w4_rows128(const GemmP& p) { return w4_use128(p); }
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
+  if (gemm_w4d_ok(p)) {
+    GemmP q = p;
+    q.group = w4_group(p.group);
+    return gemm_w4d_launch(q, b_mn, w4_use128(q), s);
+  }
   return b_mn ? launch_w4_epi<true>(p, s) : launch_w4_epi<false>(p, s);
 }
 

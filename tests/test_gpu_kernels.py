@@ -4,6 +4,7 @@ Inputs are rounded to bf16 first and the oracle runs in fp32 on the rounded valu
 tolerances measure only the kernels' own rounding (bf16 outputs: ~2^-8 relative).
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -125,7 +126,9 @@ def test_gemm_gelu_derivative_epilogues(cuda, M, N, K, act):
     assert rel_err(z.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
-def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False):
+def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
+    """Kernel gvl_gemm picks for this shape; `epi` (a test epilogue name) sets the
+    descriptor's epilogue fields the way gvl.kernels.gemm does (the routing depends on it)."""
     import ctypes as C
     from gvl import _lib
     d = _lib.GemmDesc()
@@ -133,6 +136,18 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False):
     d.m, d.n, d.k = M, N, K
     d.lda, d.ldb, d.ldc = A.stride(0), B.stride(0), N
     d.a_mn, d.b_mn = a_mn, b_mn
+    d.alpha = 1.0
+    p = A.data_ptr()  # any aligned device pointer: only the routing is asked
+    if epi in ("bias", "bias_res", "bias_act_d", "drop_res"):
+        d.bias = p
+    if epi in ("bias_res", "res_inplace", "drop_res"):
+        d.residual, d.ldr = p, N
+    if epi == "bias_act_d":
+        d.act, d.pre_out, d.ldp = 3, p, N
+    if epi in ("mul", "dact", "dact_erf"):
+        d.dact, d.pre_in, d.ldp = {"mul": 3, "dact": 1, "dact_erf": 2}[epi], p, N
+    if epi == "drop_res":
+        d.drop_p, d.seed = 0.1, 1
     if tickets:  # as gvl.kernels.gemm passes them (workspace + in-launch combine tickets)
         K_ = _k()
         ws, tk = K_._gemm_workspace(A.device), K_._gemm_tickets(A.device)
@@ -305,9 +320,9 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
     b = (torch.randn(K, N) * 0.05).to(BF)
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
-    name = _kernel_name(A, B, a_mn, b_mn, M, N, K)
-    if not a_mn and K % 192 == 0:  # K-contiguous A: the four-wave 192x128 kernel takes it
-        assert name.startswith("gemm_w4_kernel"), name
+    name = _kernel_name(A, B, a_mn, b_mn, M, N, K, epi=epi)
+    if not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
+        assert name.startswith(_w4_name(M, K, epi)), name
     else:
         assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
     h = a.float() @ b.float()
@@ -339,11 +354,25 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
 
 
+# epilogues gemm_w4d_kernel is instantiated for (gemm_w4d.h epi_supported)
+W4D_EPIS = ("plain", "bias", "bias_res", "res_inplace", "drop_res")
+
+
+def _w4_name(M, K, epi):
+    """Kernel the default four-wave routing picks (GVL_W4D unset): the direct-A variant
+    (gemm_w4d.h) when K is a multiple of six 64-deep steps and the epilogue is one of its."""
+    mode = os.environ.get("GVL_W4D", "1")
+    rows = "m" if M <= 4096 else ""
+    direct = K % 384 == 0 and epi in W4D_EPIS and mode != "0" and (mode == "2" or not rows)
+    return f"gemm_w4d{rows}_kernel" if direct else f"gemm_w4{rows}_kernel"
+
+
 @pytest.mark.parametrize("b_mn", [0, 1])
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "res_inplace", "bias_act_d", "mul", "dact_erf"])
 @pytest.mark.parametrize("M,N,K", [(8064, 768, 3072), (8064, 768, 2304), (7992, 776, 192),
                                    (16384, 768, 384), (300, 128, 192), (8064, 3072, 768),
-                                   (3968, 768, 3072), (4096, 768, 768), (3970, 776, 192)])
+                                   (3968, 768, 3072), (4096, 768, 768), (3970, 776, 192),
+                                   (7992, 776, 384), (3970, 904, 768)])
 def test_gemm_w4(cuda, b_mn, epi, M, N, K):
     """Four-wave 192x128 / 128x128 deep-ring kernel (gemm_w4.hip), forced with gvl_gemm_tune(3, 10):
     the caption decoder's N = 768 shapes (252 tiles, one per CU), ragged M and N (N % 128 != 0),
@@ -383,13 +412,14 @@ def test_gemm_w4(cuda, b_mn, epi, M, N, K):
         kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
     _lib.lib().gvl_gemm_tune(3, 10)
     try:
-        name = _kernel_name(A, B, 0, b_mn, M, N, K)
+        name = _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi)
         y = K_.gemm(A, B, a_mn=False, b_mn=bool(b_mn), **kw)
         torch.cuda.synchronize()
     finally:
         _lib.lib().gvl_gemm_tune(3, -1)
-    # 128-row tiles (gemm_w4m_kernel) where 192-row ones would fill < 3/4 of the CUs
-    assert name.startswith("gemm_w4m_kernel" if M <= 4096 else "gemm_w4_kernel"), name
+    # 128-row tiles (gemm_w4m_kernel / gemm_w4dm_kernel) where 192-row ones would fill < 3/4
+    # of the CUs; the direct-A variant where K % 384 == 0 and its epilogue is instantiated
+    assert name.startswith(_w4_name(M, K, epi)), name
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
@@ -534,7 +564,7 @@ def test_gemm_dropout_gate(cuda):
     assert 0.08 < frac < 0.12
 
 
-@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, "gemm_w4m_kernel"),
+@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, _w4_name(4096, 768, "drop_res")),
                                          (4096, 3072, 768, "gemm_pp3_kernel"),
                                          (200, 136, 72, None), (4096, 768, 3072, None)])
 def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
@@ -550,7 +580,7 @@ def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
     p, seed = 0.1, 123456789
     A, B = x.to(cuda), w.to(cuda)
     if kern is not None:
-        name = _kernel_name(A, B, 0, 0, M, N, Kd)
+        name = _kernel_name(A, B, 0, 0, M, N, Kd, epi="drop_res")
         assert name.startswith(kern), name
     y = K_.gemm(A, B, bias=bias.to(cuda), residual=res.to(cuda), drop_p=p, seed=seed)
     h = x.float() @ w.float().t() + bias.float()
