@@ -148,10 +148,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
   gemm_epilogue<4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-// GVL_GEMM_IMPL=regstage|lds|ring|pp|8p picks the kernel family (0|1|2|3|4, default 3: the
-// persistent ping-pong kernel where it fills the chip, else the 128x128 ring; 4: the
-// quadrant-phase kernel of gemm_8p.hip where K % 64 == 0, else as 3);
-// GVL_GEMM_CFG forces a tile config of that family.
+// GVL_GEMM_IMPL=regstage|lds|ring|pp picks the kernel family (0|1|2|3, default 3: the
+// four-wave kernels for narrow outputs, the persistent ping-pong kernel where it fills the
+// chip, else the 128x128 ring); GVL_GEMM_CFG forces a tile config of that family (impl 3:
+// 3 = the persistent kernel, 10 = the four-wave kernel, 11 = the default routing without it).
 struct GemmEnv {
   int impl = 3, cfg = -1, group = 8;
   GemmEnv() {
@@ -162,7 +162,6 @@ struct GemmEnv {
     if (s && s[0] == 'l') impl = 1;
     if (s && s[0] == 'r' && s[1] == 'i') impl = 2;
     if (s && s[0] == 'p') impl = 3;
-    if (s && s[0] == '8') impl = 4;
     const char* c = getenv("GVL_GEMM_CFG");
     if (c) cfg = atoi(c);
   }
@@ -209,7 +208,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 4 && cfg >= -1 && cfg <= 11, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 11, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -221,12 +220,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     GemmP p;
     fill_params(d, p);
-    GemmP q = p;
-    if (env().impl == 4 && env().cfg < 0 && gvl::gemm_8p_plan(q, false)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
-      snprintf(buf, len, "gemm_8p_kernel<%s, %s, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
-               epi[q.splits > 1 ? 0 : gvl::gemm_epi_kind(q)]);
-    } else if ((env().cfg < 0 || env().cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, env().cfg == 10)) {
+    const int cfg = env().cfg;
+    if ((cfg < 0 || cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, cfg == 10)) {
       // (cfg 11: default routing with the four-wave kernel off)
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       if (gvl::gemm_w4d_ok(p))
@@ -235,10 +230,7 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       else
         snprintf(buf, len, "%s<3, %s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
                  tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
-    } else if (env().cfg >= 0 && env().cfg != 11) {
-      snprintf(buf, len, "%s, %s, %s>", gvl::gemm_pp2_name(env().cfg == 10 ? 3 : env().cfg),
-               tf[d->a_mn != 0], tf[d->b_mn != 0]);
-    } else if (gvl::gemm_pp3_plan(p, false)) {
+    } else if (gvl::gemm_pp3_plan(p, cfg == 3 || cfg == 10)) {
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
@@ -284,13 +276,14 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
-    if (env().cfg == 10 && gvl::gemm_w4_plan(p, d->a_mn, true)) {
+    const int cfg = env().cfg;
+    GemmP q = p;
+    if (cfg == 10 && gvl::gemm_w4_plan(p, d->a_mn, true)) {
       gvl::gemm_w4_launch(p, d->b_mn, s);
-    } else if (env().cfg >= 0 && env().cfg != 11) {
-      gvl::gemm_pp2_launch(p, d->a_mn, d->b_mn, env().cfg == 10 ? 3 : env().cfg, s);
-    } else if (env().cfg != 11 && gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
-    } else if (env().impl == 4 && gvl::gemm_8p_try(p, d->a_mn, d->b_mn, false, s)) {
-    } else if (!gvl::gemm_pp3_try(p, d->a_mn, d->b_mn, s)) {
+    } else if (cfg != 11 && cfg != 3 && cfg != 10 && gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
+    } else if (gvl::gemm_pp3_plan(q, cfg == 3 || cfg == 10)) {
+      gvl::gemm_pp3_launch(q, d->a_mn, d->b_mn, s);
+    } else {
       gvl::gemm_ring_launch(p, d->a_mn, d->b_mn, gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn), s);
     }
     GVL_LAUNCH_CHECK("gvl_gemm(pp)");

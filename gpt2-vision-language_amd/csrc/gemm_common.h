@@ -174,7 +174,7 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
   }
 }
 
-// Compile-time epilogue kinds for the persistent kernels (gemm_pp2.hip): each instance
+// Compile-time epilogue kinds for the persistent kernels (gemm_pp3.h): each instance
 // carries only its own ops; EPI_GEN runs the runtime-flag path above.
 enum {
   EPI_PLAIN = 0, EPI_BIAS = 1, EPI_BIAS_RES = 2, EPI_BIAS_ACT = 3, EPI_DACT = 4, EPI_GEN = 5,
@@ -483,9 +483,7 @@ const char* gemm_ring_name(int cfg);
 bool gemm_ring_ok(const gvl_gemm_desc* d);
 int gemm_ring_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
 int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced, int a_mn);
-const char* gemm_pp2_name(int cfg);
-int gemm_pp2_launch(const GemmP& p, int a_mn, int b_mn, int cfg, hipStream_t s);
-int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels
+int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels (gemm_plan.hip)
 bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
@@ -494,8 +492,6 @@ int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);
 int gemm_pp3_launch_tf(const GemmP& p, hipStream_t s);
 int gemm_pp3_launch_tt(const GemmP& p, hipStream_t s);
 int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
-bool gemm_8p_plan(GemmP& p, bool force);
-bool gemm_8p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_rows128(const GemmP& p);  // the launch uses 128-row tiles (gemm_w4m_kernel)

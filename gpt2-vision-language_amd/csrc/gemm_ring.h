@@ -1,5 +1,5 @@
 // LDS-DMA ring helpers shared by the ring / ping-pong GEMM kernels (gemm_ring.hip,
-// gemm_pp2.hip): K-steps of 32, one slot per step, swizzle applied on the DMA source.
+// gemm_pp3.h, gemm_w4.hip): K-steps of 32, one slot per step, swizzle applied on the DMA source.
 #pragma once
 #include "common.h"
 

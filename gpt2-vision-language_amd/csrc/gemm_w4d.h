@@ -99,6 +99,12 @@ struct DImg<true> {
 #ifndef GVL_W4D_IGLP
 #define GVL_W4D_IGLP 1
 #endif
+// Timing-only diagnostic builds (wrong results; never the shipped library): GVL_W4D_DIAG=1
+// drops the in-loop A loads, 2 the in-loop B loads and LDS writes, 3 the per-step barrier.
+// GVL_W4D_EPIS_MIN instantiates only the plain and bias+residual epilogues (fast A/B builds).
+#ifndef GVL_W4D_DIAG
+#define GVL_W4D_DIAG 0
+#endif
 
 template <bool BMN, int EPI, int BM>
 __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
@@ -239,8 +245,10 @@ __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
   // it reloads B set SB with (OB, KB) and A set SA with (OA, KA)
 #define W4D_STEP(SA, SB, SL, OA, KA, OB, KB)                                                 \
   do {                                                                                       \
-    W4D_WRITE_B(SB, ((SL) + 2) % 3);                                                         \
-    W4D_LOAD_B(SB, OB, KB);                                                                  \
+    if constexpr (GVL_W4D_DIAG != 2) {                                                       \
+      W4D_WRITE_B(SB, ((SL) + 2) % 3);                                                       \
+      W4D_LOAD_B(SB, OB, KB);                                                                \
+    }                                                                                        \
     {                                                                                        \
       const char* sl_ = smem + (SL) * D_SLOT;                                                \
       _Pragma("unroll") for (int j = 0; j < FN; ++j) f1[j] = BI::frag(sl_, j, 1, lane);      \
@@ -255,9 +263,10 @@ __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
     _Pragma("unroll") for (int i = 0; i < FM; ++i)                                           \
       _Pragma("unroll") for (int j = 0; j < FN; ++j)                                         \
         acc[i][j] = mfma16(f1[j], __builtin_bit_cast(short8_t, av[SA][i][1]), acc[i][j]);    \
-    W4D_LOAD_A(SA, OA, KA);                                                                  \
+    if constexpr (GVL_W4D_DIAG != 1) W4D_LOAD_A(SA, OA, KA);                                 \
     W4D_SCHED();                                                                             \
-    barrier_lds();                                                                           \
+    if constexpr (GVL_W4D_DIAG == 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      \
+    else barrier_lds();                                                                      \
   } while (0)
 
   for (int t = 0; t < ntl; ++t) {
@@ -336,17 +345,23 @@ int launch_rows(const GemmP& p, bool rows128, hipStream_t s) {
 
 // the epilogues the caption decoders and the Q-Former route to the four-wave kernels
 inline bool epi_supported(int e) {
+#ifdef GVL_W4D_EPIS_MIN
+  return e == EPI_PLAIN || e == EPI_BIAS_RES;
+#else
   return e == EPI_PLAIN || e == EPI_BIAS || e == EPI_BIAS_RES || e == EPI_RES || e == EPI_BIAS_DROP_RES;
+#endif
 }
 
 template <bool BMN>
 int launch_epi(const GemmP& p, bool rows128, hipStream_t s) {
   switch (gvl::gemm_epi_kind(p)) {
     case EPI_PLAIN: return launch_rows<BMN, EPI_PLAIN>(p, rows128, s);
-    case EPI_BIAS: return launch_rows<BMN, EPI_BIAS>(p, rows128, s);
     case EPI_BIAS_RES: return launch_rows<BMN, EPI_BIAS_RES>(p, rows128, s);
+#ifndef GVL_W4D_EPIS_MIN
+    case EPI_BIAS: return launch_rows<BMN, EPI_BIAS>(p, rows128, s);
     case EPI_RES: return launch_rows<BMN, EPI_RES>(p, rows128, s);
     case EPI_BIAS_DROP_RES: return launch_rows<BMN, EPI_BIAS_DROP_RES>(p, rows128, s);
+#endif
     default: return -1;
   }
 }
