@@ -254,9 +254,12 @@ def flush_wgrads(task=None):
                         _ready(p)
 
 
-# Concurrent batched weight-gradient launches (flush_wgrads); GVL_WGRAD_STREAMS=0: in order on
-# the queueing stream.
-WGRAD_STREAMS = os.environ.get("GVL_WGRAD_STREAMS", "1") != "0"
+# Concurrent batched weight-gradient launches (flush_wgrads), GVL_WGRAD_STREAMS=1 (A/B knob,
+# off): measured slower — LM 837-845k vs 865k tokens/s (profiles/r3/wgrad_streams_ab_r3s2.txt).
+# Each persistent launch sizes its grid to the whole chip and walks its tiles XCD-contiguously;
+# a second one started on the CUs the first frees lands its workgroups late and off its XCD
+# map, so the tail it was meant to fill grows instead.
+WGRAD_STREAMS = os.environ.get("GVL_WGRAD_STREAMS", "0") == "1"
 _SIDE_STREAMS = {}  # device -> [streams]
 
 
