@@ -127,6 +127,12 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 // ------------------------------------------------------------------------------------
 // Short sequences (G = 1, no dropout) compile for 4 waves per SIMD (<= 128 VGPRs, no spill):
 // 4 blocks per CU instead of 3, so the caption decoder's 1536 (b, h) blocks take 1.5 rounds.
+// Timing-only diagnostic builds of the forward (wrong results; never the shipped library):
+// GVL_ATTN_FWD_DIAG=1 replaces the softmax exponentials by a multiply, 2 drops the in-loop K/V
+// loads and LDS stores, 3 drops the per-tile __syncthreads.
+#ifndef GVL_ATTN_FWD_DIAG
+#define GVL_ATTN_FWD_DIAG 0
+#endif
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void 
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + 1 < nkt;
+    const bool more = GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
     if (more) {
       load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
       load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
@@ -266,7 +272,11 @@ __global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void 
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+#if GVL_ATTN_FWD_DIAG == 1
+          const float e = fmaf(sc[g][n][r], p.c2, -msub) * 1e-3f;
+#else
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -msub));
+#endif
           if (!GVL_ATTN_FWD_V2 || DROP) ls += e;
           float pe = e;
           if constexpr (DROP) {
@@ -305,7 +315,11 @@ __global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void 
       store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
       store_rows<true>(rv, smem[(kt + 1) & 1][1], tid);
     }
+#if GVL_ATTN_FWD_DIAG == 3
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     __syncthreads();
+#endif
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
   store_rows<false>(rv, smem[0][1], tid);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + 1 < nkt;
+    const bool more = GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
     if (more) {
       load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
       load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
@@ -844,6 +858,10 @@ __global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG
 // dQ, LDS-DMA pipelined (default for Tq > 64): attn_bwd_dq_kernel with the K / V tiles moved
 // global -> LDS by buffer_load ... lds into a 3-slot ring two key tiles ahead (as
 // attn_bwd_dkdv_dma_kernel; transposed K reads by inline asm for the same reason).
+// It also computes D = rowsum(dO * O) itself (attn_bwd_pre_kernel's job): each lane already
+// holds 16 of its row's 64 dO values as MFMA fragments, loads the matching O values, and the
+// four lanes of a row reduce by two shuffles; D goes to the workspace for the dK/dV kernel
+// that runs next (one launch and a 2 x [B,H,T,64] re-read fewer).
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG gg) {
   using gvl_ring::lds_void_t;
@@ -876,8 +894,27 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     }
     const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
     lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
-    Dq[g] = qok[g] ? gg.Dws[ridx] : 0.f;
     drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
+  }
+  {  // D = rowsum(dO * O): this lane's 16 dims (2 x 8 at 32 s2 + 8 Gl), then the row's 4 lanes
+    const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float sd = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t of = load_frag_global(obase + q[g] * p.o_st, s2, lane, qok[g]);
+        const uint4 ou = __builtin_bit_cast(uint4, of), du = __builtin_bit_cast(uint4, df[g][s2]);
+        const uint32_t ow[4] = {ou.x, ou.y, ou.z, ou.w}, dw[4] = {du.x, du.y, du.z, du.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          sd += lo_bf(ow[k]) * lo_bf(dw[k]) + hi_bf(ow[k]) * hi_bf(dw[k]);
+      }
+      sd += __shfl_xor(sd, 16, 64);
+      sd += __shfl_xor(sd, 32, 64);
+      Dq[g] = qok[g] ? sd : 0.f;
+      if (qok[g] && Gl == 0) gg.Dws[(b * p.H + h) * p.Tq + q[g]] = sd;
+    }
   }
   int64_t kend = p.Tk;
   if (p.causal) {
@@ -1293,9 +1330,11 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
     GVL_LAUNCH_CHECK("gvl_attn_bwd(short)");
     return 0;
   }
-  const int64_t rows = d->B * d->H * d->Tq;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
-  GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
+  if (!dq_dma_enabled()) {  // (the LDS-DMA dQ kernel computes D itself)
+    const int64_t rows = d->B * d->H * d->Tq;
+    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
+    GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
+  }
   const int Gq = pick_groups(d->Tq);
   dim3 gq(grid_1d(d, (d->Tq + 64 * Gq - 1) / (64 * Gq)));
   if (dq_dma_enabled()) {
