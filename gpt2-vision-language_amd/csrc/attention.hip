@@ -133,8 +133,11 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 #ifndef GVL_ATTN_FWD_DIAG
 #define GVL_ATTN_FWD_DIAG 0
 #endif
+#ifndef GVL_ATTN_G4_OCC  // blocks per CU the G = 4 forward compiles for
+#define GVL_ATTN_G4_OCC 1
+#endif
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, G >= 4 ? 1 : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
+__global__ __launch_bounds__(NT, G >= 4 ? GVL_ATTN_G4_OCC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
@@ -696,8 +699,12 @@ GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
                : "memory");
 }
 
-template <bool DROP>
-__global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG gg) {
+// G key groups of 16 per wave (64 G keys per block): every Q / dO fragment read from LDS
+// (row and transposed) feeds G MFMAs.  With G = 1 a CU reads 128 KiB of fragments per block
+// and query tile against 4 x 32 MFMAs per SIMD (3 blocks: LDS and MFMA pipe both ~100 %
+// busy, PMC-free count from the MICROARCH LDS rates); G = 2 halves the LDS bytes per MFMA.
+template <int G, bool DROP>
+__global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG gg) {
   using gvl_ring::lds_void_t;
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   __shared__ __attribute__((aligned(16))) char smem[3 * DK_SLOT];
@@ -705,30 +712,37 @@ __global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Gl = lane >> 4;
   int64_t kt, h, b;
-  tile_of_block<false>(p, (p.Tk + KT - 1) / KT, kt, h, b);
-  const int64_t kblk0 = kt * KT;
+  tile_of_block<false>(p, (p.Tk + KT * G - 1) / (KT * G), kt, h, b);
+  const int64_t kblk0 = kt * KT * G;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
   const int64_t rbase = (b * p.H + h) * p.Tq;
-  const int64_t key = kblk0 + wave * 16 + (lane & 15);
-  const bool kok = key < p.Tk;
-  short8_t kf[2], vf[2];
+  int64_t key[G];
+  bool kok[G];
+  short8_t kf[G][2], vf[G][2];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    kf[s2] = load_frag_global(kbase + key * p.k_st, s2, lane, kok);
-    vf[s2] = load_frag_global(vbase + key * p.v_st, s2, lane, kok);
+  for (int g = 0; g < G; ++g) {
+    key[g] = kblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    kok[g] = key[g] < p.Tk;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      kf[g][s2] = load_frag_global(kbase + key[g] * p.k_st, s2, lane, kok[g]);
+      vf[g][s2] = load_frag_global(vbase + key[g] * p.v_st, s2, lane, kok[g]);
+    }
   }
   const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
   const int nqt = (int)((p.Tq + KT - 1) / KT);
   const int nq = nqt - qt_first;
-  float4_t dk[4], dv[4];
+  float4_t dk[G][4], dv[G][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dk[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+      dv[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    }
   // buffer resources (bounds = the last valid row's end: rows >= Tq read zero)
   const __amdgpu_buffer_rsrc_t rq = gvl_ring::uniform_rsrc(qbase, ((p.Tq - 1) * p.q_st + D) * 2);
   const __amdgpu_buffer_rsrc_t rd = gvl_ring::uniform_rsrc(dobase, ((p.Tq - 1) * gg.do_st + D) * 2);
@@ -777,51 +791,65 @@ __global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG
     const char* ds = qs + KT * D * 2;
     const float* sl = reinterpret_cast<const float*>(qs + 2 * KT * D * 2);
     const int64_t q0 = (int64_t)qt * KT;
-    float4_t sc[4], dp[4];
+    float4_t sc[G][4], dp[G][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
-      dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+        dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        sc[n] = mfma16(frag_row(qs, 16 * n, s2, lane), kf[s2], sc[n]);
-        dp[n] = mfma16(frag_row(ds, 16 * n, s2, lane), vf[s2], dp[n]);
-      }
-    }
-    const int64_t kg_max = kblk0 + wave * 16 + 15;
-    const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
-    const int qlim = (int)(p.Tq - q0), kq = (int)(key - q0);
-    float4_t pd[4];
+        const short8_t qrf = frag_row(qs, 16 * n, s2, lane), drf = frag_row(ds, 16 * n, s2, lane);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      // lse / D of this lane's 4 queries: read by inline asm, because hipcc cannot tell these
-      // bytes apart from the in-flight lse / D DMA of another slot and would drain vmcnt(0)
-      // (the whole two-ahead prefetch) before a plain read; they landed before the barrier.
-      float4_t l4, d4;
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256\n\ts_waitcnt lgkmcnt(0)"
-                   : "=v"(l4), "=v"(d4)
-                   : "v"((uint32_t)reinterpret_cast<uintptr_t>(sl + 16 * n + 4 * Gl))
-                   : "memory");
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qi = 16 * n + 4 * Gl + r;
-        const float lr = l4[r] * LOG2E;
-        const float dr = d4[r];
-        float pv = __builtin_amdgcn_exp2f(fmaf(sc[n][r], p.c2, -lr));
-        if (msk && (!kok || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
-        float pdrop = pv, dpv = dp[n][r];
-        if constexpr (DROP) {
-          const bool keep = rng_keep(
-              seed_, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key, p.drop_thresh);
-          pdrop = keep ? pv * p.drop_scale : 0.f;
-          dpv = keep ? dpv * p.drop_scale : 0.f;
+        for (int g = 0; g < G; ++g) {
+          sc[g][n] = mfma16(qrf, kf[g][s2], sc[g][n]);
+          dp[g][n] = mfma16(drf, vf[g][s2], dp[g][n]);
         }
-        pd[n][r] = pdrop;
-        sc[n][r] = pv * (dpv - dr);  // dS
       }
     }
-    const short8_t pf[2] = {pack_frag(pd[0], pd[1]), pack_frag(pd[2], pd[3])};
-    const short8_t sf[2] = {pack_frag(sc[0], sc[1]), pack_frag(sc[2], sc[3])};
+    const int qlim = (int)(p.Tq - q0);
+    short8_t pf[G][2], sf[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t kg_max = kblk0 + wave * 16 * G + g * 16 + 15;
+      const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
+      const int kq = (int)(key[g] - q0);
+      float4_t pd[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        // lse / D of this lane's 4 queries: read by inline asm, because hipcc cannot tell these
+        // bytes apart from the in-flight lse / D DMA of another slot and would drain vmcnt(0)
+        // (the whole two-ahead prefetch) before a plain read; they landed before the barrier.
+        float4_t l4, d4;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(l4), "=v"(d4)
+                     : "v"((uint32_t)reinterpret_cast<uintptr_t>(sl + 16 * n + 4 * Gl))
+                     : "memory");
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * n + 4 * Gl + r;
+          const float lr = l4[r] * LOG2E;
+          const float dr = d4[r];
+          float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lr));
+          if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
+          float pdrop = pv, dpv = dp[g][n][r];
+          if constexpr (DROP) {
+            const bool keep = rng_keep(
+                seed_, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
+            pdrop = keep ? pv * p.drop_scale : 0.f;
+            dpv = keep ? dpv * p.drop_scale : 0.f;
+          }
+          pd[n][r] = pdrop;
+          sc[g][n][r] = pv * (dpv - dr);  // dS
+        }
+      }
+      pf[g][0] = pack_frag(pd[0], pd[1]);
+      pf[g][1] = pack_frag(pd[2], pd[3]);
+      sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+      sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       short8_t dof[4], qtf[4];
@@ -832,25 +860,29 @@ __global__ __launch_bounds__(NT, 3) void attn_bwd_dkdv_dma_kernel(AttnP p, AttnG
       }
       lds_wait8(dof, qtf);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        dv[t] = mfma16(dof[t], pf[s2], dv[t]);
-        dk[t] = mfma16(qtf[t], sf[s2], dk[t]);
-      }
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          dv[g][t] = mfma16(dof[t], pf[g][s2], dv[g][t]);
+          dk[g][t] = mfma16(qtf[t], sf[g][s2], dk[g][t]);
+        }
     }
     if (i + 1 < nq) wait_tiles(i + 2 < nq ? 1 : 0);
     gvl_ring::barrier_lds();  // slot st is refilled by iteration i+1's issue
   }
-  if (kok) {
-    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + key * gg.dk_st;
-    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + key * gg.dv_st;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (!kok[g]) continue;
+    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + key[g] * gg.dk_st;
+    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + key[g] * gg.dv_st;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int d = 16 * t + 4 * Gl;
       *reinterpret_cast<uint2*>(dkr + d) =
-          make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale),
-                     pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
+          make_uint2(pack2(dk[g][t][0] * p.scale, dk[g][t][1] * p.scale),
+                     pack2(dk[g][t][2] * p.scale, dk[g][t][3] * p.scale));
       *reinterpret_cast<uint2*>(dvr + d) =
-          make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+          make_uint2(pack2(dv[g][t][0], dv[g][t][1]), pack2(dv[g][t][2], dv[g][t][3]));
     }
   }
 }
@@ -1237,14 +1269,22 @@ int pick_fwd_groups(int64_t T, bool drop) {
   return pick_groups(T);
 }
 
-// dK/dV key groups per wave: GVL_DKDV_G=2 runs 32 keys per wave (one wave per SIMD, the
-// accumulators need > 256 registers) for Tk > 64; default 1.
-int dkdv_groups(int64_t Tk) {
+bool dkdv_dma_enabled();
+
+// dK/dV key groups per wave for Tk > 64: 16 keys (G = 1).  GVL_DKDV_G=2 runs 32 keys per wave
+// on the LDS-DMA kernel (2 blocks per CU, 241 VGPRs, no dropout instance: it spills) —
+// measured no faster at T = 1024 (bwd 0.195-0.200 vs 0.191-0.197 ms,
+// profiles/r3/attn_g_ab_r3s2.txt): the halved LDS bytes per MFMA are offset by 2 instead
+// of 3 blocks per CU.
+int dkdv_groups(int64_t Tk, bool drop) {
   static const int g = [] {
     const char* e = getenv("GVL_DKDV_G");
-    return (e && atoi(e) == 2) ? 2 : 1;
+    return e ? atoi(e) : 0;
   }();
-  return (g == 2 && Tk > 64) ? 2 : 1;
+  if (Tk <= 64) return 1;
+  if (g == 1 || g == 2) return g;
+  (void)drop;
+  return 1;
 }
 
 // Single-launch backward for Tq, Tk <= 64 (attn_bwd_short_kernel); GVL_ATTN_SHORT=0 restores the
@@ -1353,13 +1393,17 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<1, false>), gq, dim3(NT), 0, s, p, g);
   }
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
-  // dK/dV keeps one 16-key group per wave: two groups need >256 VGPRs (dK and dV
-  // accumulators for 32 keys x 64 dims) and spill to scratch.
-  const int Gk = dkdv_groups(d->Tk);
+  // dK/dV: 32 keys per wave on the LDS-DMA kernel without dropout (dkdv_groups); its G = 2
+  // instance exists without dropout only
+  const int Gk = (dkdv_dma_enabled() && p.has_drop) ? 1 : dkdv_groups(d->Tk, p.has_drop != 0);
   dim3 gk(grid_1d(d, (d->Tk + 64 * Gk - 1) / (64 * Gk)));
-  if (Gk == 1 && dkdv_dma_enabled()) {
-    if (p.has_drop) gvl::launch_timed(attn_bwd_dkdv_dma_kernel<true>, gk, dim3(NT), 0, s, p, g);
-    else gvl::launch_timed(attn_bwd_dkdv_dma_kernel<false>, gk, dim3(NT), 0, s, p, g);
+  if (dkdv_dma_enabled()) {
+    if (Gk == 2) {
+      gvl::launch_timed(attn_bwd_dkdv_dma_kernel<2, false>, gk, dim3(NT), 0, s, p, g);
+    } else {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, true>, gk, dim3(NT), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, false>, gk, dim3(NT), 0, s, p, g);
+    }
   } else if (Gk == 2) {
     if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), gk, dim3(NT), 0, s, p, g);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), gk, dim3(NT), 0, s, p, g);

@@ -208,11 +208,13 @@ struct EpiKind {
 // fragment pair, each of which would also wait behind the LDS-DMA of later K-steps.
 // Lane (row l&15, column quad q) holds, per fragment (i, j), the 4 bf16 at row
 // mw0 + 16 i + (l & 15), cols nw0 + 16 j + 4 q.
-template <int FM, int FN, int EPI>
+// FULL: the whole wave tile's [M, N] operand is fetched at once, by the kernel, ahead of the
+// epilogue (gemm_w4d.h: one tile per CU, so a fetch inside the epilogue is exposed latency).
+template <int FM, int FN, int EPI, bool FULL = false>
 struct EpiPre {
   using KD = EpiKind<EPI>;
   uint2 b[KD::BIAS ? FN : 1];
-  static constexpr int XH = FM / 2;  // the [M, N] operand is fetched half a tile at a time
+  static constexpr int XH = FULL ? FM : FM / 2;  // else half a tile at a time, in the epilogue
   uint2 x[KD::AUX ? XH : 1][KD::AUX ? FN : 1];
   uint64_t seed = 0;  // effective dropout seed (DROP), read with the bias, not per element
   GVL_DEV void load_bias(const GemmP& p, int64_t nw0, int lane) {
@@ -309,9 +311,9 @@ static __device__ __forceinline__ void gemm_epi_quad(const GemmP& p, float4_t a,
 // columns: quad q stores cols 16 (j + (q & 1)) + 8 (q >> 1) .. + 7, so one store
 // instruction writes 16 rows x 64 B instead of 16 rows x 32 B.
 // Odd FN: the last fragment is stored unpaired (8-B stores).
-template <int FM, int FN, int EPI = EPI_GEN>
+template <int FM, int FN, int EPI = EPI_GEN, bool FULL = false>
 GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
-                             int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI>& pre,
+                             int64_t nw0, int lane, float alpha, EpiPre<FM, FN, EPI, FULL>& pre,
                              void* cout = nullptr, const bf16_t* res = nullptr) {
   // cout / res: this problem's C and residual in a batched launch (default p.C / p.residual)
   bf16_t* const cbase = reinterpret_cast<bf16_t*>(cout ? cout : p.C);
@@ -325,7 +327,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
   for (int i = 0; i < FM; ++i) {
     const int64_t m = mw0 + i * 16 + (lane & 15);
     const bool mok = m < p.M;
-    if (EpiKind<EPI>::AUX && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i, res);
+    if (EpiKind<EPI>::AUX && !FULL && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i, res);
 #pragma unroll
     for (int j = 0; j + 1 < FN; j += 2) {
       const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
@@ -341,7 +343,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         using KD = EpiKind<EPI>;
         const uint2 b0 = KD::BIAS ? pre.b[KD::BIAS ? j : 0] : make_uint2(0, 0);
         const uint2 b1 = KD::BIAS ? pre.b[KD::BIAS ? j + 1 : 0] : make_uint2(0, 0);
-        constexpr int XH = EpiPre<FM, FN, EPI>::XH;
+        constexpr int XH = EpiPre<FM, FN, EPI, FULL>::XH;
         const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
         const uint2 a1 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j + 1 : 0] : make_uint2(0, 0);
         if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0, pre.seed);
@@ -375,7 +377,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         float v0[4] = {0.f, 0.f, 0.f, 0.f}, h0[4] = {0.f, 0.f, 0.f, 0.f};
         using KD = EpiKind<EPI>;
         const uint2 b0 = KD::BIAS ? pre.b[KD::BIAS ? j : 0] : make_uint2(0, 0);
-        constexpr int XH = EpiPre<FM, FN, EPI>::XH;
+        constexpr int XH = EpiPre<FM, FN, EPI, FULL>::XH;
         const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
         if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0, pre.seed);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);

@@ -105,6 +105,13 @@ struct DImg<true> {
 #ifndef GVL_W4D_DIAG
 #define GVL_W4D_DIAG 0
 #endif
+// GVL_W4D_AUXPF=1: the epilogue's [M, N] operand (residual / pre_in) is fetched one step ahead
+// of the epilogue (EpiPre FULL) instead of FM / 2 rows at a time inside it — measured slower
+// (Q-Former step 15.09k vs 15.18k images/s, bias+residual GEMM 40.0-40.5 vs 39.4-39.6 us; the
+// held registers make two instances spill), so off (profiles/r3/w4d_auxpf_ab_r3s2.txt)
+#ifndef GVL_W4D_AUXPF
+#define GVL_W4D_AUXPF 0
+#endif
 
 template <bool BMN, int EPI, int BM>
 __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
@@ -188,7 +195,7 @@ __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
   tile_coords(0, cu_m0, cu_n0);
   a_offs(cu_m0, oa);
   b_offs(cu_n0, ob);
-  EpiPre<FM, FN, EPI> pre;
+  EpiPre<FM, FN, EPI, GVL_W4D_AUXPF> pre;  // bias now; the residual / pre_in tile before the last step
   pre.load_bias(p, cu_n0, lane);
 
   // prologue: B steps 0..3 (0, 1 written to slots 0, 1; sets 0, 1 reloaded with 2, 3),
@@ -292,8 +299,12 @@ __device__ __forceinline__ void gemm_w4d_body(const GemmP& p) {
       W4D_STEP(2, 0, 2, oa, k + 5, nb, 0);
       W4D_STEP(0, 1, 0, na, 0, nb, 1);
       W4D_STEP(1, 0, 1, na, 1, nb, 2);
+      // the epilogue's [M, N] operand (residual / pre_in) for this wave's outputs, one step
+      // ahead of its use instead of FM / XH exposed fetches inside the epilogue (earlier and
+      // the registers it holds make the last block spill)
+      if constexpr (EpiKind<EPI>::AUX && GVL_W4D_AUXPF) pre.load_aux(p, cu_m0 + wave * RW, cu_n0, lane, 0);
       W4D_STEP(2, 1, 2, na, 2, nb, 3);
-      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + wave * RW, cu_n0, lane, alpha, pre);
+      gemm_epilogue16<FM, FN, EPI, GVL_W4D_AUXPF>(p, acc, cu_m0 + wave * RW, cu_n0, lane, alpha, pre);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
