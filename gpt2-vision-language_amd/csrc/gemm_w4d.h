@@ -34,7 +34,7 @@
 #include "gemm_ring.h"
 #include "../../include/gvl.h"
 
-namespace gvl_w4d {
+namespace {  // (anonymous: rocprofv3 and the bench timer then report the same kernel names)
 
 using namespace gvl_ring;
 
@@ -377,4 +377,4 @@ int launch_epi(const GemmP& p, bool rows128, hipStream_t s) {
   }
 }
 
-}  // namespace gvl_w4d
+}  // namespace

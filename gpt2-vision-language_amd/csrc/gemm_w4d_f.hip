@@ -17,12 +17,12 @@ bool gemm_w4d_ok(const GemmP& p) {
     const char* e = getenv("GVL_W4D");
     return e ? atoi(e) : 1;
   }();
-  return mode != 0 && p.K % (6 * gvl_w4d::D_KS) == 0 && p.lda % 8 == 0 &&
-         gvl_w4d::epi_supported(gemm_epi_kind(p)) && (mode == 2 || !gemm_w4_rows128(p));
+  return mode != 0 && p.K % (6 * D_KS) == 0 && p.lda % 8 == 0 &&
+         epi_supported(gemm_epi_kind(p)) && (mode == 2 || !gemm_w4_rows128(p));
 }
 
 int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s) {
-  return b_mn ? gemm_w4d_launch_t(p, rows128, s) : gvl_w4d::launch_epi<false>(p, rows128, s);
+  return b_mn ? gemm_w4d_launch_t(p, rows128, s) : launch_epi<false>(p, rows128, s);
 }
 
 }  // namespace gvl

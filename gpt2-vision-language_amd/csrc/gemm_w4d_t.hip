@@ -3,6 +3,6 @@
 
 namespace gvl {
 int gemm_w4d_launch_t(const GemmP& p, bool rows128, hipStream_t s) {
-  return gvl_w4d::launch_epi<true>(p, rows128, s);
+  return launch_epi<true>(p, rows128, s);
 }
 }  // namespace gvl
