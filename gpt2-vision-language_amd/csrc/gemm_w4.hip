@@ -489,8 +489,11 @@ bool gemm_w4_rows128(const GemmP& p) { return w4_use128(p); }
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
   if (gemm_w4d_ok(p)) {
+    // direct-A tiles walk all column tiles of a row block before the next one, so an XCD reads
+    // each A row block once: HBM bytes per Q-Former dX launch 104 -> 80 MB at equal time
+    // (profiles/r3/w4d_group_ab_r3s2.txt); GVL_W4_GROUP overrides
     GemmP q = p;
-    q.group = w4_group(p.group);
+    q.group = w4_group(1);
     return gemm_w4d_launch(q, b_mn, w4_use128(q), s);
   }
   return b_mn ? launch_w4_epi<true>(p, s) : launch_w4_epi<false>(p, s);
