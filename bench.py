@@ -44,9 +44,17 @@ def setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GVL_BENCH_ONE_DEVICE=1: rehearsal of the N > 1 path on a one-GPU box — every rank on
+    # cuda:0, collectives over gloo (RCCL refuses two ranks on one device).  Never a bench line.
+    one_device = os.environ.get("GVL_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if one_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     return world, rank, torch.device(f"cuda:{local}")
 
 
@@ -195,7 +203,8 @@ def _quiet(fn):
 
 def graphed(step, warmup):
     """Capture the step into hipGraphs (gvl.graph) after `warmup` eager steps: one graph at
-    N=1; at N>1 two graphs around one eager RCCL all-reduce of the grad arena."""
+    N=1; at N>1 the last micro-step's backward in segments, each its own graph, with the
+    buckets a segment finalised all-reduced on RCCL's stream while the next segment runs."""
     from gvl.graph import GraphedStep
     model, opt, batches, loss_fn, lr_fn = step.graph_args
     gs = GraphedStep(model, opt, batches, loss_fn, lr_fn(0), warmup=warmup,
