@@ -47,6 +47,6 @@ def test_traffic_table_from_counter_csvs(tmp_path):
 def test_committed_traffic_covers_bench_dominant_kernels():
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         t = json.load(f)["workloads"]
-    # the dominant GEMMs of the round-2 bench lines (profiles/r2/r2h/bench_default_r2h.json)
+    # the dominant GEMMs of the round-3 bench lines (profiles/r3/bench_r3s2.json)
     assert t["lm"]["gemm_pp3_kernel<4, false, true, 0, 192, 256>"]["hbm_bytes"] > 0
-    assert t["qf"]["gemm_w4_kernel<3, true, 0>"]["hbm_bytes"] > 0
+    assert t["qf"]["gemm_w4d_kernel<true, 0>"]["hbm_bytes"] > 0
