@@ -110,18 +110,26 @@ class QFormerLayer(nn.Module):
                               bf(mha.out_proj.weight), bf(mha.out_proj.bias), residual,
                               mha.num_heads, self_attn, p_attn, p_out, seed)
 
-    def _ln(self, ln, x):
-        return Fn.LayerNormFn.apply(x, bf(ln.weight), bf(ln.bias), ln.eps)
+    def _ln(self, ln, x, tape=None):
+        return Fn.LayerNormFn.apply(x, bf(ln.weight), bf(ln.bias), ln.eps, tape)
 
     def forward(self, q, v):
-        q2 = self._ln(self.ln1, q)
-        q = self._mha(self.self_attn, q2, q2, q, True)
-        q = self._mha(self.cross_attn, self._ln(self.ln2_q, q), self._ln(self.ln2_v, v), q, False)
-        q2 = self._ln(self.ln3, q)
+        # q -> q + f(LN(q)) three times: each unit takes q detached as its residual and a
+        # Fn.ResTape carries the output gradient to the LayerNorm backward of the same q, so
+        # q's two gradients are summed inside that launch (no autograd add kernels)
+        t = Fn.ResTape()
+        q2 = self._ln(self.ln1, q, t)
+        q = Fn.ResTapFn.apply(self._mha(self.self_attn, q2, q2, q.detach(), True), t)
+        t = Fn.ResTape()
+        q = Fn.ResTapFn.apply(self._mha(self.cross_attn, self._ln(self.ln2_q, q, t),
+                                        self._ln(self.ln2_v, v), q.detach(), False), t)
+        t = Fn.ResTape()
+        q2 = self._ln(self.ln3, q, t)
         p = self.drop.p if self.training else 0.0
         fc1, fc2 = self.mlp[0], self.mlp[2]
-        return Fn.MLPFn.apply(q2, bf(fc1.weight), bf(fc1.bias), bf(fc2.weight), bf(fc2.bias), q,
-                              2, p, new_seed() if p > 0 else 0)
+        return Fn.ResTapFn.apply(
+            Fn.MLPFn.apply(q2, bf(fc1.weight), bf(fc1.bias), bf(fc2.weight), bf(fc2.bias),
+                           q.detach(), 2, p, new_seed() if p > 0 else 0), t)
 
 
 class BLIP2Bridge(nn.Module):

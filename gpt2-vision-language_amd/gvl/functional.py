@@ -492,9 +492,36 @@ class GPTBlockFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------- LayerNorm
+class ResTape:
+    """Pre-LN residual stream x -> x + f(LN(x)) outside one fused unit (the Q-Former layers):
+    autograd would sum x's two gradients (the residual path's and LN's) with a separate add
+    kernel.  Instead the unit gets x detached as its residual, ResTapFn on its output hands
+    d(output) to this tape, and LayerNormFn(x, ..., tape) returns dx = d(output) + LN'(dy) from
+    one LayerNorm-backward launch (gvl_layernorm_bwd_res)."""
+    __slots__ = ("d",)
+
+    def __init__(self):
+        self.d = None
+
+
+class ResTapFn(torch.autograd.Function):
+    """Identity on a residual unit's output; its backward stores the output gradient in the
+    tape (the gradient of the unit's detached residual input) and passes it on unchanged."""
+
+    @staticmethod
+    def forward(ctx, y, tape):
+        ctx.tape = tape
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ctx.tape.d = dy
+        return dy, None
+
+
 class LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, eps: float = 1e-5):
+    def forward(ctx, x, w, b, eps: float = 1e-5, tape: ResTape = None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if x2.dtype != BF16:
@@ -505,6 +532,7 @@ class LayerNormFn(torch.autograd.Function):
             ctx.save_for_backward(x2, w, mean, rstd)
             ctx.shp = shp
             ctx.params = (w, b)
+            ctx.tape = tape
             _mark(ctx)
         return y.view(shp)
 
@@ -514,13 +542,17 @@ class LayerNormFn(torch.autograd.Function):
         C = x2.shape[1]
         d2 = dy.reshape(-1, C).to(BF16).contiguous()
         dx = torch.empty(x2.shape[0], C, dtype=BF16, device=x2.device)
+        res = None
+        if ctx.tape is not None and ctx.tape.d is not None:  # the stream's residual gradient
+            res = ctx.tape.d.reshape(-1, C).to(BF16).contiguous()
+            ctx.tape.d = None
         if _need(ctx, 1) or _need(ctx, 2):
             dw, db = _ln_bwd(ctx, 1, 2, ctx.params[0], ctx.params[1], d2, x2, mean, rstd, dx,
-                             False)
+                             False, residual=res)
         else:
             dw = db = None
-            K.layernorm_bwd(d2, x2, w, mean, rstd, dx=dx)
-        return (dx.view(ctx.shp) if _need(ctx, 0) else None), dw, db, None
+            K.layernorm_bwd(d2, x2, w, mean, rstd, dx=dx, residual=res)
+        return (dx.view(ctx.shp) if _need(ctx, 0) else None), dw, db, None, None
 
 
 # ---------------------------------------------------------------------------- Linear

@@ -35,15 +35,35 @@ def accumulate(model, optimizer, micro_batches, loss_fn, buckets: GradBuckets = 
     optimizer.zero_grad()
     loss_accum = None
     for i, batch in enumerate(micro_batches):
-        loss = loss_fn(model, batch) / accum
+        loss = loss_fn(model, batch)
+        # loss/accum without the division kernels: backward is seeded with a cached 1/accum
+        # scalar (no ones-fill, no div forward/backward per micro-step) and the running mean
+        # is one scaled add
         la = loss.detach().float()
-        loss_accum = la if loss_accum is None else loss_accum + la
+        if loss_accum is None:
+            loss_accum = la if accum == 1 else la * (1.0 / accum)
+        else:
+            loss_accum = loss_accum.add(la, alpha=1.0 / accum)
         if buckets is not None:
             buckets.set_sync(i == accum - 1)
-        loss.backward()
+        loss.backward(_grad_seed(loss, accum))
     if buckets is not None:
         buckets.wait()
     return loss_accum
+
+
+_SEEDS = {}
+
+
+def _grad_seed(loss, accum):
+    """d(loss/accum)/d(loss) as a cached device scalar of loss's dtype (created once, so a
+    captured step replays no fill for it)."""
+    key = (loss.device, loss.dtype, accum)
+    t = _SEEDS.get(key)
+    if t is None:
+        t = torch.full((), 1.0 / accum, dtype=loss.dtype, device=loss.device)
+        _SEEDS[key] = t
+    return t
 
 
 def finish(optimizer, lr, max_norm: float = 1.0):
