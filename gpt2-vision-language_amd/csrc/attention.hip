@@ -9,11 +9,12 @@
 // The output accumulator keeps the same query on the lane, so rescales are lane-local.
 // With G = 2 every K/V fragment read from LDS feeds two MFMAs (two query groups).
 //
-// Backward (FA2 recompute, no atomics, deterministic): a preprocess kernel computes
-// D = rowsum(dO*O); dQ is produced by a query-tile kernel looping over key tiles and
-// dK/dV by a key-tile kernel (G groups of 16 keys per wave) looping over query tiles.
-// P is recomputed from the saved log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash
-// mask on (b,h,q,k), identical in every kernel.
+// Backward (FA2 recompute, no atomics, deterministic): dQ by a query-tile kernel looping over
+// key tiles, which also computes D = rowsum(dO*O) for the next one; dK/dV by a key-tile
+// kernel (16 keys per wave) looping over query tiles; both stage their streamed tiles by
+// LDS-DMA.  Sequences of <= 64 rows take one fused kernel.  P is recomputed from the saved
+// log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash mask on (b,h,q,k), identical in
+// every kernel.
 #include <algorithm>
 
 #include "common.h"
@@ -133,11 +134,8 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 #ifndef GVL_ATTN_FWD_DIAG
 #define GVL_ATTN_FWD_DIAG 0
 #endif
-#ifndef GVL_ATTN_G4_OCC  // blocks per CU the G = 4 forward compiles for
-#define GVL_ATTN_G4_OCC 1
-#endif
 template <int G, bool DROP>
-__global__ __launch_bounds__(NT, G >= 4 ? GVL_ATTN_G4_OCC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
+__global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel(AttnP p) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
   __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
@@ -346,326 +344,10 @@ __global__ __launch_bounds__(NT, G >= 4 ? GVL_ATTN_G4_OCC : ((G == 1 && !DROP) ?
   (void)l;
 }
 
-// ------------------------------------------------------------------------------------
-// D[b,h,q] = sum_d dO*O  (one thread per row, 8 x 16-B loads each)
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = p.B * p.H * p.Tq;
-  if (idx >= total) return;
-  const int64_t q = idx % p.Tq, bh = idx / p.Tq, h = bh % p.H, b = bh / p.H;
-  const bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q * p.o_st;
-  const bf16_t* drow = g.dout + b * g.do_sb + h * g.do_sh + q * g.do_st;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const uint4 a = *reinterpret_cast<const uint4*>(orow + c * 8);
-    const uint4 d = *reinterpret_cast<const uint4*>(drow + c * 8);
-    s += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
-         hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
-         lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
-  }
-  g.Dws[idx] = s;
-}
-
-// dQ: block = (64*G-query tile, head, batch), each wave G groups of 16 query rows.
-template <int G, bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnP p, AttnG gg) {
-  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
-  constexpr int QT = 64 * G;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Gl = lane >> 4;
-  int64_t qt, h, b;
-  tile_of_block<true>(p, (p.Tq + QT - 1) / QT, qt, h, b);
-  const int64_t qblk0 = qt * QT;
-  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
-  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
-  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
-  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
-  int64_t q[G];
-  bool qok[G];
-  short8_t qf[G][2], df[G][2];
-  float lse2[G], Dq[G];
-  uint64_t drow[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
-    qok[g] = q[g] < p.Tq;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      qf[g][s] = load_frag_global(qbase + q[g] * p.q_st, s, lane, qok[g]);
-      df[g][s] = load_frag_global(dobase + q[g] * gg.do_st, s, lane, qok[g]);
-    }
-    const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
-    lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
-    Dq[g] = qok[g] ? gg.Dws[ridx] : 0.f;
-    drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
-  }
-
-  int64_t kend = p.Tk;
-  if (p.causal) {
-    const int64_t lim = qblk0 + QT;
-    if (lim < kend) kend = lim;
-  }
-  const int nkt = (int)((kend + KT - 1) / KT);
-  float4_t acc[G][4];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  uint4 rk[2], rv[2];
-  load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
-  load_rows(rv, vbase, p.v_st, 0, p.Tk, tid);
-  store_rows<false>(rk, smem[0][0], tid);
-  store_rows<false>(rv, smem[0][1], tid);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
-    if (more) {
-      load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
-      load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
-    }
-    const char* ks = smem[kt & 1][0];
-    const char* vs = smem[kt & 1][1];
-    const int64_t k0 = (int64_t)kt * KT;
-    float4_t sc[G][4], dp[G][4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
-        dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const short8_t kf = frag_row(ks, 16 * n, s, lane);
-        const short8_t vf = frag_row(vs, 16 * n, s, lane);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          sc[g][n] = mfma16(kf, qf[g][s], sc[g][n]);
-          dp[g][n] = mfma16(vf, df[g][s], dp[g][n]);
-        }
-      }
-    }
-    short8_t sf[G][2];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      // rows past Tq and keys past Tk meet zero Q/dO/K/V rows, so only the causal diagonal
-      // and the ragged last key tile need the explicit mask (wave-uniform test)
-      const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
-      const bool msk = k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0);
-      const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kk = 16 * n + 4 * Gl + r;
-          float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lse2[g]));
-          if (msk && (kk >= kl || (p.causal && kk > ql))) pv = 0.f;
-          float dpv = dp[g][n][r];
-          if constexpr (DROP)
-            dpv = rng_keep(seed_, drow[g] + (uint64_t)(k0 + kk), p.drop_thresh) ? dpv * p.drop_scale : 0.f;
-          sc[g][n][r] = pv * (dpv - Dq[g]);  // dS
-        }
-      sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
-      sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const short8_t kf = frag_tr<false>(ks, t, s, lane);
-#pragma unroll
-        for (int g = 0; g < G; ++g) acc[g][t] = mfma16(kf, sf[g][s], acc[g][t]);
-      }
-    }
-    if (more) {
-      store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
-      store_rows<false>(rv, smem[(kt + 1) & 1][1], tid);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (!qok[g]) continue;
-    bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + q[g] * gg.dq_st;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int d = 16 * t + 4 * Gl;
-      *reinterpret_cast<uint2*>(dst + d) =
-          make_uint2(pack2(acc[g][t][0] * p.scale, acc[g][t][1] * p.scale),
-                     pack2(acc[g][t][2] * p.scale, acc[g][t][3] * p.scale));
-    }
-  }
-}
-
-// dK/dV: block = (64*G-key tile, head, batch), waves own G groups of 16 keys; loop over
-// 64-query tiles staged in LDS (Q, dO read both by rows and transposed).
-template <int G, bool DROP>
-__global__ __launch_bounds__(NT, G == 1 ? 3 : 1) void attn_bwd_dkdv_kernel(AttnP p, AttnG gg) {
-  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
-  constexpr int KB = 64 * G;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][Q,dO]
-  __shared__ __attribute__((aligned(16))) float sl[2][2][KT];         // [stage][lse2, D]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Gl = lane >> 4;
-  int64_t kt, h, b;
-  tile_of_block<false>(p, (p.Tk + KB - 1) / KB, kt, h, b);
-  const int64_t kblk0 = kt * KB;
-  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
-  const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
-  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
-  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
-  const int64_t rbase = (b * p.H + h) * p.Tq;
-  int64_t key[G];
-  bool kok[G];
-  short8_t kf[G][2], vf[G][2];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    key[g] = kblk0 + wave * 16 * G + g * 16 + (lane & 15);
-    kok[g] = key[g] < p.Tk;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      kf[g][s] = load_frag_global(kbase + key[g] * p.k_st, s, lane, kok[g]);
-      vf[g][s] = load_frag_global(vbase + key[g] * p.v_st, s, lane, kok[g]);
-    }
-  }
-  const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
-  const int nqt = (int)((p.Tq + KT - 1) / KT);
-  float4_t dk[G][4], dv[G][4];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      dk[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
-      dv[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
-    }
-  if (qt_first < nqt) {
-    uint4 rq[2], rd[2];
-    float rl = 0.f, rD = 0.f;
-    auto fetch = [&](int qt) {
-      const int64_t q0 = (int64_t)qt * KT;
-      load_rows(rq, qbase, p.q_st, q0, p.Tq, tid);
-      load_rows(rd, dobase, gg.do_st, q0, p.Tq, tid);
-      if (tid < KT) {
-        const int64_t qq = q0 + tid;
-        rl = qq < p.Tq ? p.lse[rbase + qq] * LOG2E : 0.f;
-        rD = qq < p.Tq ? gg.Dws[rbase + qq] : 0.f;
-      }
-    };
-    auto put = [&](int st) {
-      store_rows<false>(rq, smem[st][0], tid);
-      store_rows<false>(rd, smem[st][1], tid);
-      if (tid < KT) {
-        sl[st][0][tid] = rl;
-        sl[st][1][tid] = rD;
-      }
-    };
-    fetch(qt_first);
-    put(0);
-    __syncthreads();
-    for (int qt = qt_first; qt < nqt; ++qt) {
-      const int st = (qt - qt_first) & 1;
-      const bool more = qt + 1 < nqt;
-      if (more) fetch(qt + 1);
-      const char* qs = smem[st][0];
-      const char* ds = smem[st][1];
-      const int64_t q0 = (int64_t)qt * KT;
-      float4_t sc[G][4], dp[G][4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
-          dp[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const short8_t qfr = frag_row(qs, 16 * n, s, lane);
-          const short8_t dfr = frag_row(ds, 16 * n, s, lane);
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            sc[g][n] = mfma16(qfr, kf[g][s], sc[g][n]);
-            dp[g][n] = mfma16(dfr, vf[g][s], dp[g][n]);
-          }
-        }
-      }
-      // lane holds S[q = q0 + 16n + 4Gl + r][key[g]]; lse and D of those 4 consecutive
-      // queries come from LDS as one float4 each
-      short8_t pf[G][2], sf[G][2];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int64_t kg_max = kblk0 + wave * 16 * G + g * 16 + 15;
-        const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
-        const int qlim = (int)(p.Tq - q0), kq = (int)(key[g] - q0);
-        float4_t pd[4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          // lse / D of this lane's 4 queries, read where used (register budget: 3 waves/SIMD)
-          const float4 l4 = *reinterpret_cast<const float4*>(&sl[st][0][16 * n + 4 * Gl]);
-          const float4 d4 = *reinterpret_cast<const float4*>(&sl[st][1][16 * n + 4 * Gl]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int qi = 16 * n + 4 * Gl + r;
-            const float lr = r == 0 ? l4.x : r == 1 ? l4.y : r == 2 ? l4.z : l4.w;
-            const float dr = r == 0 ? d4.x : r == 1 ? d4.y : r == 2 ? d4.z : d4.w;
-            float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lr));
-            if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
-            float pdrop = pv, dpv = dp[g][n][r];
-            if constexpr (DROP) {
-              const bool keep = rng_keep(
-                  seed_, (uint64_t)(rbase + q0 + qi) * (uint64_t)p.Tk + (uint64_t)key[g], p.drop_thresh);
-              pdrop = keep ? pv * p.drop_scale : 0.f;
-              dpv = keep ? dpv * p.drop_scale : 0.f;
-            }
-            pd[n][r] = pdrop;
-            sc[g][n][r] = pv * (dpv - dr);  // dS
-          }
-        }
-        pf[g][0] = pack_frag(pd[0], pd[1]);
-        pf[g][1] = pack_frag(pd[2], pd[3]);
-        sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
-        sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const short8_t dot = frag_tr<false>(ds, t, s, lane);
-          const short8_t qtr = frag_tr<false>(qs, t, s, lane);
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            dv[g][t] = mfma16(dot, pf[g][s], dv[g][t]);
-            dk[g][t] = mfma16(qtr, sf[g][s], dk[g][t]);
-          }
-        }
-      }
-      if (more) put(st ^ 1);  // stage st^1 was last read in iteration qt-1
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (!kok[g]) continue;
-    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + key[g] * gg.dk_st;
-    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + key[g] * gg.dv_st;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int d = 16 * t + 4 * Gl;
-      *reinterpret_cast<uint2*>(dkr + d) =
-          make_uint2(pack2(dk[g][t][0] * p.scale, dk[g][t][1] * p.scale),
-                     pack2(dk[g][t][2] * p.scale, dk[g][t][3] * p.scale));
-      *reinterpret_cast<uint2*>(dvr + d) =
-          make_uint2(pack2(dv[g][t][0], dv[g][t][1]), pack2(dv[g][t][2], dv[g][t][3]));
-    }
-  }
-}
-
-// dK/dV, LDS-DMA pipelined (default for Tk > 64): as attn_bwd_dkdv_kernel<1, DROP>, but the
-// Q / dO tiles and their lse / D rows move global -> LDS by buffer_load ... lds (no staging
-// registers) into a 3-slot ring, two query tiles ahead of the one being computed, with counted
-// vmcnt waits (PMC of the register-staged kernel: waves waiting 48 % of their cycles, LDS 5 %:
+// dK/dV, LDS-DMA pipelined (Tk > 64): block = (64-key tile, head, batch); the Q / dO tiles
+// and their lse / D rows move global -> LDS by buffer_load ... lds (no staging registers)
+// into a 3-slot ring, two query tiles ahead of the one being computed, with counted
+// vmcnt waits (PMC of the round-2 register-staged kernel: waves waiting 48 % of their cycles, LDS 5 %:
 // the one-tile-ahead register prefetch did not cover the load latency).  The DMA writes each
 // 64x64 tile lane-linearly in 1-KiB pieces (8 rows of 128 B); the swz_tr XOR is applied to
 // the source chunk, so the image is the same as store_rows'.  Rows past Tq read zero (buffer
@@ -887,10 +569,10 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
   }
 }
 
-// dQ, LDS-DMA pipelined (default for Tq > 64): attn_bwd_dq_kernel with the K / V tiles moved
-// global -> LDS by buffer_load ... lds into a 3-slot ring two key tiles ahead (as
+// dQ, LDS-DMA pipelined (Tq > 64): block = (64*G-query tile, head, batch), each wave G groups
+// of 16 query rows; the K / V tiles move global -> LDS by buffer_load ... lds into a 3-slot ring two key tiles ahead (as
 // attn_bwd_dkdv_dma_kernel; transposed K reads by inline asm for the same reason).
-// It also computes D = rowsum(dO * O) itself (attn_bwd_pre_kernel's job): each lane already
+// It also computes D = rowsum(dO * O) itself (round 3; a separate launch before): each lane already
 // holds 16 of its row's 64 dO values as MFMA fragments, loads the matching O values, and the
 // four lanes of a row reduce by two shuffles; D goes to the workspace for the dK/dV kernel
 // that runs next (one launch and a 2 x [B,H,T,64] re-read fewer).
@@ -1258,59 +940,12 @@ int pick_groups(int64_t T) {
   return T > 64 ? 2 : 1;
 }
 
-// Forward query groups per wave: GVL_ATTN_FWD_G=4 runs 64 query rows per wave (one wave per
-// SIMD: K/V fragments read from LDS once per 64 rows instead of 32) when Tq > 128, no dropout.
-int pick_fwd_groups(int64_t T, bool drop) {
-  static const int g4 = [] {
-    const char* e = getenv("GVL_ATTN_FWD_G");
-    return e ? atoi(e) : 0;
-  }();
-  if (g4 == 4 && T > 128 && !drop) return 4;
-  return pick_groups(T);
-}
-
-bool dkdv_dma_enabled();
-
-// dK/dV key groups per wave for Tk > 64: 16 keys (G = 1).  GVL_DKDV_G=2 runs 32 keys per wave
-// on the LDS-DMA kernel (2 blocks per CU, 241 VGPRs, no dropout instance: it spills) —
-// measured no faster at T = 1024 (bwd 0.195-0.200 vs 0.191-0.197 ms,
-// profiles/r3/attn_g_ab_r3s2.txt): the halved LDS bytes per MFMA are offset by 2 instead
-// of 3 blocks per CU.
-int dkdv_groups(int64_t Tk, bool drop) {
-  static const int g = [] {
-    const char* e = getenv("GVL_DKDV_G");
-    return e ? atoi(e) : 0;
-  }();
-  if (Tk <= 64) return 1;
-  if (g == 1 || g == 2) return g;
-  (void)drop;
-  return 1;
-}
-
 // Single-launch backward for Tq, Tk <= 64 (attn_bwd_short_kernel); GVL_ATTN_SHORT=0 restores the
 // three-kernel path (A/B measurement).
 bool short_bwd_enabled() {
   static const bool on = [] {
     const char* e = getenv("GVL_ATTN_SHORT");
     return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// LDS-DMA pipelined dQ and dK/dV (attn_bwd_dq_dma_kernel, attn_bwd_dkdv_dma_kernel);
-// GVL_DKDV_DMA=0 restores the register-staged kernels (A/B).
-bool dkdv_dma_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("GVL_DKDV_DMA");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-bool dq_dma_enabled() {  // GVL_DQ_DMA=0: register-staged dQ kernel beside the DMA dK/dV one
-  static const bool on = [] {
-    const char* e = getenv("GVL_DQ_DMA");
-    return dkdv_dma_enabled() && !(e && e[0] == '0');
   }();
   return on;
 }
@@ -1323,12 +958,10 @@ unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntil
 extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   AttnP p;
   if (fill(d, p)) return -1;
-  const int G = pick_fwd_groups(d->Tq, p.has_drop != 0);
+  const int G = pick_groups(d->Tq);
   dim3 grid(grid_1d(d, (d->Tq + 64 * G - 1) / (64 * G)));
   hipStream_t s = gvl::as_stream(stream);
-  if (G == 4) {
-    gvl::launch_timed(attn_fwd_kernel<4, false>, grid, dim3(NT), 0, s, p);
-  } else if (G == 2) {
+  if (G == 2) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
   } else {
@@ -1370,47 +1003,22 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
     GVL_LAUNCH_CHECK("gvl_attn_bwd(short)");
     return 0;
   }
-  if (!dq_dma_enabled()) {  // (the LDS-DMA dQ kernel computes D itself)
-    const int64_t rows = d->B * d->H * d->Tq;
-    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
-    GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
-  }
+  // dQ (+ D = rowsum(dO * O) into the workspace), then dK/dV reading D
   const int Gq = pick_groups(d->Tq);
   dim3 gq(grid_1d(d, (d->Tq + 64 * Gq - 1) / (64 * Gq)));
-  if (dq_dma_enabled()) {
-    if (Gq == 2) {
-      if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<2, true>, gq, dim3(NT), 0, s, p, g);
-      else gvl::launch_timed(attn_bwd_dq_dma_kernel<2, false>, gq, dim3(NT), 0, s, p, g);
-    } else {
-      if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<1, true>, gq, dim3(NT), 0, s, p, g);
-      else gvl::launch_timed(attn_bwd_dq_dma_kernel<1, false>, gq, dim3(NT), 0, s, p, g);
-    }
-  } else if (Gq == 2) {
-    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), gq, dim3(NT), 0, s, p, g);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), gq, dim3(NT), 0, s, p, g);
+  if (Gq == 2) {
+    if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<2, true>, gq, dim3(NT), 0, s, p, g);
+    else gvl::launch_timed(attn_bwd_dq_dma_kernel<2, false>, gq, dim3(NT), 0, s, p, g);
   } else {
-    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<1, true>), gq, dim3(NT), 0, s, p, g);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<1, false>), gq, dim3(NT), 0, s, p, g);
+    if (p.has_drop) gvl::launch_timed(attn_bwd_dq_dma_kernel<1, true>, gq, dim3(NT), 0, s, p, g);
+    else gvl::launch_timed(attn_bwd_dq_dma_kernel<1, false>, gq, dim3(NT), 0, s, p, g);
   }
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dq)");
-  // dK/dV: 32 keys per wave on the LDS-DMA kernel without dropout (dkdv_groups); its G = 2
-  // instance exists without dropout only
-  const int Gk = (dkdv_dma_enabled() && p.has_drop) ? 1 : dkdv_groups(d->Tk, p.has_drop != 0);
-  dim3 gk(grid_1d(d, (d->Tk + 64 * Gk - 1) / (64 * Gk)));
-  if (dkdv_dma_enabled()) {
-    if (Gk == 2) {
-      gvl::launch_timed(attn_bwd_dkdv_dma_kernel<2, false>, gk, dim3(NT), 0, s, p, g);
-    } else {
-      if (p.has_drop) gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, true>, gk, dim3(NT), 0, s, p, g);
-      else gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, false>, gk, dim3(NT), 0, s, p, g);
-    }
-  } else if (Gk == 2) {
-    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), gk, dim3(NT), 0, s, p, g);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), gk, dim3(NT), 0, s, p, g);
-  } else {
-    if (p.has_drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, true>), gk, dim3(NT), 0, s, p, g);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, false>), gk, dim3(NT), 0, s, p, g);
-  }
+  // dK/dV: 16 keys per wave (32 measured no faster at T = 1024: 2 instead of 3 blocks per CU,
+  // profiles/r3/attn_g_ab_r3s2.txt)
+  dim3 gk(grid_1d(d, (d->Tk + 63) / 64));
+  if (p.has_drop) gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, true>, gk, dim3(NT), 0, s, p, g);
+  else gvl::launch_timed(attn_bwd_dkdv_dma_kernel<1, false>, gk, dim3(NT), 0, s, p, g);
   GVL_LAUNCH_CHECK("gvl_attn_bwd(dkdv)");
   return 0;
 }
