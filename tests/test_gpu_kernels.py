@@ -693,6 +693,17 @@ def test_attention_dropout_exact_mask(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False, drop_p=0.1, seed=4242)
 
 
+def test_attention_bwd_repeats_over_nan_filled_memory(cuda):
+    """The dropout case (40 queries x 130 keys) 12 times, the caching allocator's free memory
+    filled with NaN before each: a backward that reads any byte it did not write, or races,
+    shows up as an intermittent dQ / dK / dV error (round 3: a dQ kernel computing D itself
+    failed 4 of 40 such repeats; tools/r3/attn_stress.py)."""
+    for it in range(12):
+        junk = torch.full((32 << 20,), float("nan"), device=cuda)
+        del junk
+        _attn_case(cuda, 2, 2, 40, 130, False, packed=False, drop_p=0.1, seed=4242 + it)
+
+
 def test_attention_matches_reference_fixture(cuda, golden):
     """SDPA fixtures produced by the reference's torch path (tools/make_fixtures.py)."""
     K_ = _k()
