@@ -11,8 +11,11 @@
 
 namespace {
 
-constexpr int CE_NT = 512;
-constexpr int CE_MAXC = 16;
+#ifndef GVL_CE_NT  // threads per row (A/B: 1024 holds 8 chunks per thread instead of 16)
+#define GVL_CE_NT 512
+#endif
+constexpr int CE_NT = GVL_CE_NT;
+constexpr int CE_MAXC = 8192 / CE_NT;  // 16-B chunks per thread: V <= 65536
 constexpr float CE_L2E = 1.4426950408889634f;
 
 // bf16 -inf in columns [nvalid, 8) of an 8-column chunk (exp2 of it is exactly 0, so the
