@@ -104,3 +104,30 @@ def test_caption_batch_semantics():
         assert (y[b, n:] == 50256).all()
     lab = caption_labels(y, m)
     assert ((lab == -100) == ~m).all()
+
+
+def test_residual_tape_hands_the_branch_gradient_over():
+    """gvl.functional.ResTapFn (the Q-Former residual streams): identity forward; its backward
+    stores the output gradient in the tape — the gradient of the unit's detached residual input
+    that LayerNormFn(x, ..., tape) adds — and passes it on unchanged."""
+    from gvl import functional as F
+    tape = F.ResTape()
+    x = torch.randn(3, 4, requires_grad=True)
+    y = F.ResTapFn.apply(x * 2.0, tape)
+    assert torch.equal(y, x * 2.0) and tape.d is None
+    g = torch.randn(3, 4)
+    y.backward(g)
+    assert torch.equal(tape.d, g)
+    assert torch.allclose(x.grad, 2.0 * g)
+
+
+def test_backward_seed_is_cached_per_accumulation():
+    """gvl.train seeds loss.backward() with one cached 1/accum scalar per (device, dtype, accum),
+    so a captured step replays no fill kernel for it."""
+    from gvl import train as T
+    loss = torch.tensor(2.0, requires_grad=True)
+    s4 = T._grad_seed(loss, 4)
+    assert s4 is T._grad_seed(loss, 4) and float(s4) == 0.25
+    assert float(T._grad_seed(loss, 1)) == 1.0
+    (loss * 3.0).backward(s4)
+    assert float(loss.grad) == 0.75
