@@ -153,7 +153,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmP p) {
 // chip, else the 128x128 ring); GVL_GEMM_CFG forces a tile config of that family (impl 3:
 // 3 = the persistent kernel, 10 = the four-wave kernel, 11 = the default routing without it).
 struct GemmEnv {
-  int impl = 3, cfg = -1, group = 8;
+  int impl = 3, cfg = -1, group = 0;  // group 0: by shape (gemm_group)
   GemmEnv() {
     const char* gr = getenv("GVL_GEMM_GROUP");
     if (gr && atoi(gr) > 0) group = atoi(gr);
@@ -169,6 +169,21 @@ struct GemmEnv {
 GemmEnv& env() {
   static GemmEnv e;
   return e;
+}
+
+// Tile rows per L2 group of the tile walk (gemm_tile_of).  GVL_GEMM_WALK_RULE (A/B, build
+// time): 0 = 8 everywhere; 1 = 4 for M >= 12288 (the LM's 16384-token GEMMs), else 8;
+// 2 (default) = 4 for M or K >= 12288 (also the LM's weight gradients over 16384 tokens), else
+// 8 — LM step 856k -> 862k tokens/s, Q-Former unchanged (profiles/r3/gemm_walk_group_ab_r3s2.txt).
+// GVL_GEMM_GROUP=n overrides it for every GEMM.
+#ifndef GVL_GEMM_WALK_RULE
+#define GVL_GEMM_WALK_RULE 2
+#endif
+int gemm_group(const gvl_gemm_desc* d) {
+  if (env().group > 0) return env().group;
+  if (GVL_GEMM_WALK_RULE == 1 && d->m >= 12288) return 4;
+  if (GVL_GEMM_WALK_RULE == 2 && (d->m >= 12288 || d->k >= 12288)) return 4;
+  return 8;
 }
 
 void fill_params(const gvl_gemm_desc* d, GemmP& p) {
@@ -196,7 +211,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.bn = 256;
   p.bm = 256;
   p.kper = d->k;
-  p.group = env().group;
+  p.group = gemm_group(d);
   p.ws = (d->workspace && gvl::aligned16(d->workspace) && d->n % 4 == 0)
              ? static_cast<float*>(d->workspace) : nullptr;
   p.ws_bytes = p.ws ? d->workspace_bytes : 0;
