@@ -451,6 +451,7 @@ def main():
         "step_mfma_frac": round(value * flop_per_unit / 1e12 / PEAK_BF16_TFLOPS / world, 4),
         "loss": round(res[0], 5), "grad_norm": round(res[1], 5),
         "hip_graph": use_graph,
+        "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
         "roofline": roof,
     }
     if args.workload == "lm" and not args.no_secondary:
@@ -459,6 +460,7 @@ def main():
         for kind in args.captions.split(","):
             if not kind:
                 continue
+            torch.cuda.reset_peak_memory_stats(dev)
             cstep, cunits, ccfg = run_caption(kind, args, world, rank, dev)
             ctimer = None if args.no_kernel_pass else K.KernelTimer()
             cdt, cres = timed(cstep, args.caption_steps, 3, world, ctimer, graph=use_graph,
@@ -470,6 +472,7 @@ def main():
                 step_mfma_frac=round(cval * CAP_FLOP_PER_IMAGE[kind] / 1e12 / PEAK_BF16_TFLOPS
                                      / world, 4),
                 loss=round(cres[0], 5), config=ccfg,
+                peak_hbm_gib=round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
                 roofline=dominant_kernel(ctimer.summary(), kind, steps=3) if ctimer else None)
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 line["cpu_baseline"] = cpu_baseline(kind, seconds=args.cpu_seconds / 2)
