@@ -359,6 +359,10 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
   GemmP p;
   fill_params(&d[0], p);
   for (int i = 0; i < GVL_MAX_BATCH; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
+  float* const ws = p.ws;  // kept for the two-way split below
+  const int64_t ws_bytes = p.ws_bytes;
+  uint32_t* const tickets = p.tickets;
+  const int nticket = p.nticket;
   p.ws = nullptr;  // whole-K tiles: the batch fills the chip
   p.ws_bytes = 0;
   p.tickets = nullptr;
@@ -382,6 +386,40 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
     p.bn = e192 > e256 ? 192 : 256;
     p.tiles_m = (int)tm;
     p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
+    // Two-way K split combined in-launch (gemm_pp3_kernel: per-problem fp32 partial slabs in
+    // the workspace, tickets per tile and wave; bias gradients by gvl_colsum_batched after
+    // it, since the fused row sums would need their own combine) when the batch's
+    // whole-K tiles leave most CUs idle through one long round: the 12 attn.c_proj weight
+    // gradients (768 x 768, K = 16384) are 144 tiles of 256 x 192 on 256 CUs; split, 216
+    // half-K 256 x 256 items.  Estimate as in the planner (gemm_plan.hip): rounds x (32-deep
+    // K-steps + 6), a 192-wide step counted 0.75 / 0.9, ~4 for the combine; required >= 10 %
+    // better.  GVL_BATCHED_SPLIT=0 turns it off (A/B).
+    static const bool split_on = [] {
+      const char* e = getenv("GVL_BATCHED_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    const int64_t tn256 = (p.N + 255) / 256, items2 = 2 * (int64_t)count * tm * tn256;
+    const int64_t need = (int64_t)count * 2 * p.M * p.N * 4;
+    if (split_on && ws && tickets && p.K % 64 == 0 && p.K / 2 >= 256 &&
+        (int64_t)count * tm * tn256 * 8 <= nticket && need <= ws_bytes &&
+        (!dbias || gvl_colsum_batched_workspace_size(count, p.K, p.M) <= ws_bytes)) {
+      auto est = [&](int64_t items, double steps, double w) {
+        return (double)((items + cus - 1) / cus) * (steps + 6.0) * w;
+      };
+      const double t1 = est((int64_t)count * p.tiles_m * p.tiles_n, p.K / 32.0,
+                            p.bn == 192 ? 0.75 / 0.9 : 1.0);
+      const double t2 = est(items2, p.K / 64.0, 1.0) + 4.0;
+      if (t2 < 0.9 * t1) {
+        p.bn = 256;
+        p.tiles_n = (int)tn256;
+        p.splits = 2;
+        p.kper = p.K / 2;
+        p.ws = ws;
+        p.ws_bytes = ws_bytes;
+        p.tickets = tickets;
+        p.nticket = nticket;
+      }
+    }
   } else {
     GVL_REQUIRE(!dbias, "gvl_gemm_batched_dbias: shape not batchable (use gvl_colsum)");
     for (int i = 0; i < count; ++i) {
@@ -392,6 +430,11 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
   }
   gvl::gemm_pp3_launch(p, d[0].a_mn, d[0].b_mn, gvl::as_stream(stream));
   GVL_LAUNCH_CHECK("gvl_gemm_batched");
+  if (dbias && p.splits == 2) {  // dbias[i] += column sums of dY_i = A_i stored [K][M]
+    const void* xs[GVL_MAX_BATCH];
+    for (int i = 0; i < count; ++i) xs[i] = d[i].a;
+    return gvl_colsum_batched(xs, dbias, count, p.K, p.M, d[0].lda, 1, ws, stream);
+  }
   return 0;
 }
 

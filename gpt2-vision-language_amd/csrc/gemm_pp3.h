@@ -157,13 +157,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
   EpiPre<FM, FN, EPI> pre;
   pre.load_bias(p, cu_n0 + bcol, lane);
-  if constexpr (DB) do_db = p.batch > 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
+  if constexpr (DB) do_db = p.batch > 1 && p.splits == 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
 #define GVL_PP3_EPILOGUE()                                                                   \
   do {                                                                                       \
     bool epi_ = true;                                                                        \
     if (p.splits == 2 && p.tickets != nullptr) { /* two-way split-K combined in-launch */    \
-      const int tile_ = (int)(cu_m0 / BM) * p.tiles_n + (int)(cu_n0 / BN);                   \
-      const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws, p.ws_bytes);                      \
+      /* batched: problem bi's tickets follow problem bi-1's, its partials ws[bi][2][M][N] */   \
+      const int tile_ = (cu_bi * p.tiles_m + (int)(cu_m0 / BM)) * p.tiles_n + (int)(cu_n0 / BN); \
+      const int64_t pofs_ = (int64_t)cu_bi * 2 * p.M * p.N;                                  \
+      const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws + pofs_, p.ws_bytes - pofs_ * 4);   \
       epi_ = gemm_splitk_arrive<FM, FN>(p, acc, cu_sp, tile_, wave, cu_m0 + arow,            \
                                         cu_n0 + bcol, lane, rw);                             \
       if (epi_) gemm_splitk_gather<FM, FN>(p, acc, cu_sp, cu_m0 + arow, cu_n0 + bcol, lane, rw); \
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
       ++cu_t;
       tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
       pre.load_bias(p, cu_n0 + bcol, lane);
-      if constexpr (DB) do_db = p.batch > 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
+      if constexpr (DB) do_db = p.batch > 1 && p.splits == 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
     }
     const char* sl = smem + (c % NS) * SLOT;
 #pragma unroll

@@ -102,6 +102,8 @@ GEMM_TICKETS = 1 << 16
 # In-launch two-way split-K combine (gvl.h ABI v5 tickets): measured slower than whole-K
 # tiles on the caption step's N = 768 GEMMs, so off unless GVL_PP3_COMBINE=1.
 SPLIT_COMBINE = os.environ.get("GVL_PP3_COMBINE", "0") == "1"
+# Batched weight gradients may use it (gvl_gemm_batched decides; GVL_BATCHED_SPLIT=0: never).
+BATCHED_SPLIT = os.environ.get("GVL_BATCHED_SPLIT", "1") != "0"
 
 
 def _gemm_tickets(device):
@@ -245,7 +247,10 @@ def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
             d.residual, d.ldr = out.data_ptr(), out.stride(0)
         if ws is None:
             ws = _gemm_workspace(a.device)
+            tk = _gemm_tickets(a.device) if BATCHED_SPLIT else None
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+        if tk is not None:  # the library may split a batch that underfills the chip in two
+            d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
     if dbias is not None:
         for t in dbias:
             if t.dtype != BF16 or not t.is_contiguous():

@@ -547,11 +547,15 @@ def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
 
 @pytest.mark.parametrize("count,M,N,K,acc", [(12, 768, 768, 4096, True), (12, 2304, 768, 2048, True),
                                              (3, 3072, 768, 1024, False), (2, 200, 136, 96, True),
-                                             (17, 256, 256, 64, True)])
+                                             (17, 256, 256, 64, True), (12, 768, 768, 16384, True),
+                                             (12, 768, 768, 1024, False)])
 def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
     """gvl_gemm_batched: `count` weight-gradient GEMMs dW_i (+)= dY_i^T X_i (both operands
     MN-contiguous, as the deferred GPT-2 block weight gradients) in one persistent launch;
-    each equals its own reference.  count 17 (> 16) and a ragged shape exercise the fallback."""
+    each equals its own reference.  count 17 (> 16) and a ragged shape exercise the fallback.
+    12 x (768, 768) — the LM's attn.c_proj at K = 16384 and shorter — runs as a two-way K
+    split combined in-launch, with the fused bias row sums combined through the workspace;
+    the second (dbias) launch also checks that the first left the tickets at zero."""
     K_ = _k()
     torch.manual_seed(count + M + N + K)
     dys = [torch.randn(K, M).to(BF) for _ in range(count)]
