@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libgvl_<name>.so: the shipped objects with SEVERAL sources recompiled under extra -D
 # flags (A/B of compile-time kernel variants spanning files; load it with GVL_LIB=...).
-# usage: tools/r3/build_variant2.sh name "-DFOO=1 ..." src1.hip src2.hip ...
+# usage: tools/build_variant.sh name "-DFOO=1 ..." src1.hip src2.hip ...
 set -e
 R=$(cd "$(dirname "$0")/../.." && pwd)
 NAME=$1; FLAGS=$2; shift 2

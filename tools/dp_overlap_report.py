@@ -1,10 +1,10 @@
-"""From a rocprofv3 run with --kernel-trace --marker-trace of tools/r3/dp_overlap_trace.py
+"""From a rocprofv3 run with --kernel-trace --marker-trace of tools/dp_overlap_trace.py
 (GVL_TRACE_BUCKETS=1): for the last optimizer step, when each gradient bucket's all-reduce was
 issued (roctx marker) relative to the backward's GEMM / attention kernels — how many backward
 kernels still ran after the first and after each bucket issue.  (At world size 1 RCCL runs no
 kernel for an in-place AVG, so the issue points are the evidence; at N > 1 the all-reduce
 runs on RCCL's stream from that point while those kernels run.)
-python tools/r3/dp_overlap_report.py <out_dir>"""
+python tools/dp_overlap_report.py <out_dir>"""
 import csv
 import glob
 import sys

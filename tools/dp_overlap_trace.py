@@ -2,8 +2,8 @@
 (GradBuckets(force=True)), for a rocprofv3 kernel trace that shows the bucket all-reduces
 overlapping the backward GEMMs: eager (block-group flushes) and the captured step (segment
 graphs, buckets issued between replays).  Run under rocprofv3 --kernel-trace, then
-tools/r3/dp_overlap_report.py on the trace.
-python tools/r3/dp_overlap_trace.py [eager|graph]"""
+tools/dp_overlap_report.py on the trace.
+python tools/dp_overlap_trace.py [eager|graph]"""
 import os
 import socket
 import sys

@@ -1,7 +1,7 @@
 """Q-Former-step decoder GEMMs at M = 8064 (B = 128 x 63 rows): libgvl with the model's exact
 epilogue, the same GEMM with a plain epilogue, and torch.mm (hipBLASLt) as a yardstick.
 Interleaved rounds in one process (median of 5 rounds x 20 launches), HIP events.
-python tools/r3/gemm_diag.py [M]"""
+python tools/gemm_diag.py [M]"""
 import os
 import statistics
 import sys
