@@ -701,7 +701,7 @@ def test_attention_bwd_repeats_over_nan_filled_memory(cuda):
     """The dropout case (40 queries x 130 keys) 12 times, the caching allocator's free memory
     filled with NaN before each: a backward that reads any byte it did not write, or races,
     shows up as an intermittent dQ / dK / dV error (round 3: a dQ kernel computing D itself
-    failed 4 of 40 such repeats; tools/r3/attn_stress.py)."""
+    failed 4 of 40 such repeats; tools/attn_stress.py)."""
     for it in range(12):
         junk = torch.full((32 << 20,), float("nan"), device=cuda)
         del junk
