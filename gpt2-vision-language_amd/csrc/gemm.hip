@@ -400,9 +400,15 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
     }();
     const int64_t tn256 = (p.N + 255) / 256, items2 = 2 * (int64_t)count * tm * tn256;
     const int64_t need = (int64_t)count * 2 * p.M * p.N * 4;
+    // a split batch's bias gradients go to gvl_colsum_batched after the GEMM: every one of its
+    // preconditions is checked here, before anything is launched, so it cannot fail once the
+    // GEMM has added into C (a failure then would make the caller redo the weight gradients)
+    bool colsum_ok = gvl_colsum_batched_workspace_size(count, p.K, p.M) <= ws_bytes &&
+                     p.M % 8 == 0 && d[0].lda % 8 == 0;
+    for (int i = 0; dbias && colsum_ok && i < count; ++i)
+      colsum_ok = dbias[i] != nullptr && gvl::aligned16(d[i].a);
     if (split_on && ws && tickets && p.K % 64 == 0 && p.K / 2 >= 256 &&
-        (int64_t)count * tm * tn256 * 8 <= nticket && need <= ws_bytes &&
-        (!dbias || gvl_colsum_batched_workspace_size(count, p.K, p.M) <= ws_bytes)) {
+        (int64_t)count * tm * tn256 * 8 <= nticket && need <= ws_bytes && (!dbias || colsum_ok)) {
       auto est = [&](int64_t items, double steps, double w) {
         return (double)((items + cus - 1) / cus) * (steps + 6.0) * w;
       };
@@ -433,7 +439,9 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
   if (dbias && p.splits == 2) {  // dbias[i] += column sums of dY_i = A_i stored [K][M]
     const void* xs[GVL_MAX_BATCH];
     for (int i = 0; i < count; ++i) xs[i] = d[i].a;
-    return gvl_colsum_batched(xs, dbias, count, p.K, p.M, d[0].lda, 1, ws, stream);
+    // preconditions checked above: a failure here is a launch error, reported as -2 (never the
+    // -1 "nothing launched, use the unfused path" answer)
+    if (gvl_colsum_batched(xs, dbias, count, p.K, p.M, d[0].lda, 1, ws, stream) != 0) return -2;
   }
   return 0;
 }

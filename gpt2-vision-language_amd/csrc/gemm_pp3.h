@@ -23,6 +23,11 @@ using namespace gvl_ring;
 // Split-K: work item w = (tile w / splits, K-slice w % splits), every slice kper deep (the
 // host only splits when K divides evenly); slices store fp32 partials, gemm_splitk_reduce
 // applies the epilogue.  KC = 1, bf16 output.
+// Timing-only diagnostic builds (wrong results; never the shipped library): GVL_PP3_DIAG=1
+// stores the plain accumulators (no epilogue operands, math or side output), 2 stores nothing.
+#ifndef GVL_PP3_DIAG
+#define GVL_PP3_DIAG 0
+#endif
 template <int BN, bool BMN>
 struct SlabB {
   using type = Step<256, BMN, 8>;
@@ -175,8 +180,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     }                                                                                        \
     if (epi_) {                                                                              \
       void* c_ = p.batch > 1 ? p.Cb[cu_bi] : p.C;                                           \
-      gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_,   \
-                                   p.batch > 1 ? static_cast<const bf16_t*>(c_) : p.residual); \
+      if constexpr (GVL_PP3_DIAG == 1) {                                                     \
+        EpiPre<FM, FN, EPI_PLAIN> pp_;                                                       \
+        gemm_epilogue16<FM, FN, EPI_PLAIN>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha,  \
+                                           pp_, c_, nullptr);                                \
+      } else if constexpr (GVL_PP3_DIAG == 2) {                                              \
+        _Pragma("unroll") for (int i_ = 0; i_ < FM; ++i_)                                    \
+          _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                                  \
+            asm volatile("" ::"v"(acc[i_][j_]));                                             \
+      } else {                                                                               \
+        gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_, \
+                                     p.batch > 1 ? static_cast<const bf16_t*>(c_) : p.residual); \
+      }                                                                                      \
     }                                                                                        \
     if constexpr (DB) {                                                                      \
       if (do_db && (lane >> 4) == 0) {                                                       \

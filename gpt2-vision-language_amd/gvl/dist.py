@@ -260,10 +260,31 @@ class BackwardSegments:
         saved, self._saved = self._saved, []
         self.armed = False
         loss.backward()
+        # An input read by several cuts (the projected image tokens every Q-Former layer reads)
+        # is back-propagated once, from the lowest cut that reads it, with the gradients of
+        # every cut above summed into it: back-propagating it per segment would run its
+        # producer's backward (vis_proj) in two graph tasks, so its bucket would count as final
+        # (and be all-reduced) before the second partial gradient landed.
+        lowest = {}
+        for j, pairs in enumerate(saved):
+            for x, _ in pairs:
+                lowest.setdefault(id(x), j)
+        carry = {}
         for j in range(len(saved) - 1, -1, -1):
             if between is not None:
                 between(len(saved) - 1 - j)
-            outs = [(x, leaf.grad) for x, leaf in saved[j] if leaf.grad is not None]
+            outs = []
+            for x, leaf in saved[j]:
+                g = leaf.grad
+                if id(x) in carry:
+                    c = carry.pop(id(x))
+                    g = c if g is None else g + c
+                if g is None:
+                    continue
+                if lowest[id(x)] < j:
+                    carry[id(x)] = g
+                else:
+                    outs.append((x, g))
             if outs:
                 torch.autograd.backward([x for x, _ in outs], [g for _, g in outs])
         return len(saved) + 1

@@ -201,18 +201,10 @@ def flush_wgrads(task=None):
         key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
                dy2.device, st)
         groups.setdefault(key, []).append((p, g, dy2, x2))
-    # One persistent launch per shape leaves CUs idle in its last round of tiles (12 GPT-2
-    # blocks: 144-576 tiles on 256 CUs).  The shapes' launches write disjoint gradients, so
-    # with WGRAD_STREAMS they run on side streams forked from the queueing stream and joined
-    # back before any grad-ready hook fires (a bucket may span several shapes): the next
-    # launch's workgroups take the CUs the previous one's last round leaves free.  The queued
-    # operands stay referenced until after the join, so their memory is not reused early.
     order = list(groups.items())
-    side = _wgrad_streams(order) if WGRAD_STREAMS and len(order) > 1 else None
     ready = []
-    for gi, (key, items) in enumerate(order):
-        st = key[-1] if side is None else side[gi]
-        with torch.cuda.stream(st):
+    for key, items in order:
+        with torch.cuda.stream(key[-1]):
             for i in range(0, len(items), 16):
                 chunk = items[i:i + 16]
                 bias = [paired.pop(_dkey(d), None) for _, _, d, _ in chunk]
@@ -228,16 +220,9 @@ def flush_wgrads(task=None):
                 ready += [p for p, *_ in chunk]
                 if fused:
                     ready += [b[0] for b in bias]
-        if side is None:
-            for p in ready:
-                _ready(p)
-            ready = []
-    if side is not None:
-        for key, _ in order:  # join: every queueing stream waits for every side stream
-            for s2 in side:
-                key[-1].wait_stream(s2)
         for p in ready:
             _ready(p)
+        ready = []
     for k, (p, g) in paired.items():  # (unreachable unless a weight entry vanished)
         raise RuntimeError(f"gvl: unpaired deferred bias gradient {k}")
     if rest_b:
@@ -252,32 +237,6 @@ def flush_wgrads(task=None):
                                      accumulate=True)
                     for p, *_ in chunk:
                         _ready(p)
-
-
-# Concurrent batched weight-gradient launches (flush_wgrads), GVL_WGRAD_STREAMS=1 (A/B knob,
-# off): measured slower — LM 837-845k vs 865k tokens/s (profiles/r3/wgrad_streams_ab_r3s2.txt).
-# Each persistent launch sizes its grid to the whole chip and walks its tiles XCD-contiguously;
-# a second one started on the CUs the first frees lands its workgroups late and off its XCD
-# map, so the tail it was meant to fill grows instead.
-WGRAD_STREAMS = os.environ.get("GVL_WGRAD_STREAMS", "0") == "1"
-_SIDE_STREAMS = {}  # device -> [streams]
-
-
-def _wgrad_streams(order):
-    """One stream per shape group: the first is the group's own queueing stream, the others
-    are side streams (created once per device, reused) that first wait for it."""
-    base = order[0][0][-1]
-    dev = base.device
-    pool = _SIDE_STREAMS.setdefault(dev, [])
-    while len(pool) < len(order) - 1:
-        pool.append(torch.cuda.Stream(device=dev))
-    out = [base]
-    for gi in range(1, len(order)):
-        s2 = pool[gi - 1]
-        for key, _ in order:
-            s2.wait_stream(key[-1])
-        out.append(s2)
-    return out
 
 
 def _final_flush(task):

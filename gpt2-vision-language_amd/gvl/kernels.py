@@ -256,7 +256,10 @@ def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
             if t.dtype != BF16 or not t.is_contiguous():
                 raise ValueError("gvl.gemm_batched: dbias must be contiguous bf16")
         da = (C.c_void_p * n)(*[t.data_ptr() for t in dbias])
-        return _L().gvl_gemm_batched_dbias(arr, da, n, _stream()) == 0
+        rc = _L().gvl_gemm_batched_dbias(arr, da, n, _stream())
+        if rc not in (0, -1):  # -1: nothing launched, the caller runs the unfused pair
+            _lib.check(rc, "gvl_gemm_batched_dbias")
+        return rc == 0
     _lib.check(_L().gvl_gemm_batched(arr, n, _stream()), "gvl_gemm_batched")
     return True
 

@@ -99,8 +99,9 @@ int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream)
 /* As gvl_gemm_batched for weight gradients (a_mn = b_mn = 1, residual == c) that also add
  * each problem's bias gradient: dbias[i] (bf16 [m]) += row sums of A_i^T over k, i.e. the
  * column sums of dY — the nn.Linear bias grad beside its weight grad, computed from the same
- * operand tiles (no second pass over dY).  Returns an error when the batch cannot run as one
- * launch (the caller then uses gvl_gemm_batched + gvl_colsum_batched). */
+ * operand tiles (no second pass over dY).  Returns -1 when the batch cannot run fused and
+ * nothing was launched (the caller then uses gvl_gemm_batched + gvl_colsum_batched); any other
+ * non-zero return is a launch failure after the GEMM may have added into C (fatal). */
 int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
                            gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):

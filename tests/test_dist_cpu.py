@@ -337,3 +337,55 @@ def test_gloo_buckets_overlap_backward(segmented):
     for g0, g1, r in zip(out[0][4], out[1][4], ref):
         assert torch.allclose(torch.from_numpy(g0), torch.from_numpy(g1))
         assert torch.allclose(torch.from_numpy(g0), r, atol=1e-6)
+
+
+class _SharedInputLayer(torch.nn.Module):
+    """A Q-Former-like layer: reads the running queries and a shared second input."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(8, 8)
+        self.b = torch.nn.Linear(8, 8)
+
+    def forward(self, q, v):
+        return q + torch.tanh(self.a(q) + self.b(v).mean(1, keepdim=True))
+
+
+class _SharedInputBridge(torch.nn.Module):
+    def __init__(self, n_layers):
+        super().__init__()
+        torch.manual_seed(3)
+        self.proj = torch.nn.Linear(8, 8)
+        self.q0 = torch.nn.Parameter(torch.randn(4, 8))
+        self.layers = torch.nn.ModuleList([_SharedInputLayer() for _ in range(n_layers)])
+
+    def forward(self, x):
+        v = self.proj(x)
+        q = self.q0.unsqueeze(0).expand(x.shape[0], -1, -1)
+        for layer in self.layers:
+            q = layer(q, v)
+        return q
+
+
+@pytest.mark.parametrize("n_layers", [2, 3, 4])
+def test_backward_segments_shared_input_backpropagated_once(n_layers):
+    """Every cut reads the projected image tokens v (gpt2_q_former/model.py:166-167).  The
+    segmented backward must give the plain backward's gradients AND run the projection's
+    backward exactly once — with >= 3 layers a per-segment backward of v used to deliver
+    vis_proj's gradient in two graph tasks, so its DP bucket fired on the first partial."""
+    import gvl.dist as D
+    x = torch.randn(2, 5, 8, generator=torch.Generator().manual_seed(1))
+    ref = _SharedInputBridge(n_layers)
+    (ref(x) ** 2).sum().backward()
+    m = _SharedInputBridge(n_layers)
+    fired = []
+    for name, p in m.named_parameters():
+        p.register_post_accumulate_grad_hook(lambda p, name=name: fired.append(name))
+    segs = D.BackwardSegments(list(m.layers)[1:])  # segment_cuts() of a Q-Former bridge
+    assert len(segs.cuts) == n_layers - 1
+    segs.arm(True)
+    loss = (m(x) ** 2).sum()
+    assert segs.backward(loss) == n_layers
+    for (name, p), pr in zip(m.named_parameters(), ref.parameters()):
+        assert torch.allclose(p.grad, pr.grad, atol=1e-6), name
+        assert fired.count(name) == 1, (name, fired)

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests.helpers import TINY, recipe_params
+from tests.helpers import TINY, margins_out, recipe_params
 
 pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
@@ -38,11 +38,15 @@ def _gpt(dev, cfg=CFG4):
     return m.to(dev).to(BF)
 
 
-def _qformer(dev):
+def _qformer(dev, n_layers=2):
+    import copy
+
     import gvl.caption as cap
     import gvl.gpt2 as g2
     lm = cap.GPT_previous(g2.GPTConfig(**TINY))
     m = cap.QFormerCaption(enc_dim=TINY["n_embd"], lm=lm, m_vis_tokens=32)
+    while len(m.bridge.layers) < n_layers:  # deeper bridges: every layer reads the image tokens
+        m.bridge.layers.append(copy.deepcopy(m.bridge.layers[-1]))
     sd = m.state_dict()
     P = recipe_params([(k, tuple(v.shape)) for k, v in sd.items()])
     m.load_state_dict({k: (P[k] if k in P else v) for k, v in sd.items()})
@@ -128,12 +132,14 @@ def test_overlap_eager_buckets_fire_during_backward(cuda):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["lm", "qformer"])
+@pytest.mark.parametrize("kind", ["lm", "qformer", "qformer3"])
 def test_segmented_graph_step_matches_eager(cuda, kind):
     """The captured DP step (segment graphs + buckets issued between replays), world size 1
     over RCCL: the buckets are logged into the segments that finalise them, and the replayed
     step's loss and gradients equal the eager bucketed train_step's on the same weights (the
-    tied wte's two contributions are summed in another order: close, not bitwise)."""
+    tied wte's two contributions are summed in another order: close, not bitwise).
+    qformer3: a 3-layer bridge, two cuts that both read the projected image tokens — vis_proj's
+    gradient must be back-propagated once, in the last segment (BackwardSegments.backward)."""
     from gvl.dist import GradBuckets
     from gvl.graph import GraphedStep
     from gvl.train import train_step
@@ -141,7 +147,8 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         mbs, loss_fn, build = _lm_batches(cuda, 3, seed=11), LM_LOSS, lambda: _gpt(cuda)
         cuts = lambda m: [m.transformer.h[2]]  # noqa: E731
     else:
-        mbs, loss_fn, build = _cap_batches(cuda, 2, seed=21), CAP_LOSS, lambda: _qformer(cuda)
+        nl = 3 if kind == "qformer3" else 2
+        mbs, loss_fn, build = _cap_batches(cuda, 2, seed=21), CAP_LOSS, lambda: _qformer(cuda, nl)
         cuts = lambda m: list(m.bridge.layers)[1:]  # noqa: E731
     _world1(cuda)
     try:
@@ -155,7 +162,7 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         b = GradBuckets(opt, bucket_mb=0.05, model=m, force=True)
         gs = GraphedStep(m, opt, mbs, loss_fn, 1e-3, warmup=2, buckets=b, segmented=True,
                          cuts=cuts(m))
-        assert gs.dp and len(gs.graphs) == 2
+        assert gs.dp and len(gs.graphs) == (3 if kind == "qformer3" else 2)
         logged = [len(x) for x in gs.logs]
         print("buckets per segment", logged, "of", len(b.buckets))
         assert logged[0] >= 1 and sum(logged) == len(b.buckets)
@@ -254,12 +261,19 @@ def test_two_ranks_gloo_match_single_process(cuda, kind, graphed):
         res = train_step(m, opt, mbs, loss_fn, 1e-3)
     print(f"{kind} graphed={graphed}: DP loss {l0:.6f} single {res.loss.item():.6f}; norm "
           f"{n0:.5f} vs {res.norm.item():.5f}")
-    assert l0 == pytest.approx(res.loss.item(), rel=2e-3)
-    assert n0 == pytest.approx(res.norm.item(), rel=3e-2)
+    lrel = abs(l0 - res.loss.item()) / abs(res.loss.item())
+    nrel = abs(n0 - res.norm.item()) / abs(res.norm.item())
     worst = (0.0, "")
     for n, p in m.named_parameters():
         if p.requires_grad:
             a = p.grad.detach().float().cpu().numpy()
             worst = max(worst, (float(np.linalg.norm(a - p0[n]) / max(np.linalg.norm(a), 1e-30)), n))
     print("worst gradient rel-L2 vs the single process", worst)
+    margins_out(f"dp2_{kind}_{'graphed' if graphed else 'eager'}",
+                {"loss_rel": lrel, "norm_rel": nrel, "worst_grad_rel": worst[0], "worst_grad": worst[1]})
+    # eager: both losses are computed before any update from identical weights, so they differ
+    # only by the order of the bf16/fp32 reductions; the graphed step's loss is the replay's,
+    # i.e. after the warm-up step's update, whose Adam-normalised gradient noise moves it more
+    assert lrel < (2e-3 if graphed else 1e-5), lrel
+    assert nrel < (3e-2 if graphed else 1e-2), nrel
     assert worst[0] < (2e-2 if graphed else 1e-2), worst

@@ -3,7 +3,7 @@
 # flags (A/B of compile-time kernel variants spanning files; load it with GVL_LIB=...).
 # usage: tools/build_variant.sh name "-DFOO=1 ..." src1.hip src2.hip ...
 set -e
-R=$(cd "$(dirname "$0")/../.." && pwd)
+R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; FLAGS=$2; shift 2
 C=$R/gpt2-vision-language_amd/csrc; B=$R/build/gvl; V=$R/build/var_$NAME
 mkdir -p $V

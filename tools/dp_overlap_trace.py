@@ -11,7 +11,7 @@ import sys
 import torch
 import torch.distributed as dist
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gpt2-vision-language_amd")]
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "eager"
