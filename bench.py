@@ -265,16 +265,21 @@ def timed(step, steps, warmup, world, timer=None, graph=False, kernel_steps=1):
 TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
 
 
-def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC passes of the same bench
-    command (tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs,
-    FETCH_SIZE doubled per the gfx950 correction); None when not measured."""
+def pmc_record(workload, kernel):
+    """The committed PMC passes of the same bench command for `kernel` (tools/pmc_traffic.sh:
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / MFMA-busy + GRBM in separate runs): HBM bytes per
+    launch (FETCH_SIZE doubled per the gfx950 correction), MFMA-busy fraction and achieved
+    clock; {} when not measured."""
     try:
         with open(TRAFFIC_FILE) as f:
             t = json.load(f)["workloads"][{"lm": "lm", "qformer": "qf"}[workload]]
-        return t[kernel]["hbm_bytes"]
+        return t[kernel]
     except (OSError, KeyError, ValueError):
-        return None
+        return {}
+
+
+def pmc_traffic(workload, kernel):
+    return pmc_record(workload, kernel).get("hbm_bytes")
 
 
 def dominant_kernel(summary, workload="lm", steps=1):
@@ -289,11 +294,16 @@ def dominant_kernel(summary, workload="lm", steps=1):
     table = [dict(kernel=k, launches_per_step=round(v["launches"] / steps, 2),
                   ms_per_step=round(v["ms"] / steps, 3),
                   avg_us=round(v["ms"] / v["launches"] * 1e3, 2),
-                  frac=round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4))
+                  frac=round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                  mfma_busy=pmc_record(workload, k).get("mfma_busy"),
+                  clock_ghz=pmc_record(workload, k).get("clock_ghz"),
+                  traffic=pmc_record(workload, k).get("hbm_bytes"))
              for k, v in top]
     return dict(kernel=name, bound="mfma", achieved=round(achieved, 1), peak=PEAK_BF16_TFLOPS,
                 unit="TFLOP/s", frac=round(achieved / PEAK_BF16_TFLOPS, 4),
                 traffic=pmc_traffic(workload, name), traffic_unit="bytes/launch",
+                mfma_busy=pmc_record(workload, name).get("mfma_busy"),
+                clock_ghz=pmc_record(workload, name).get("clock_ghz"),
                 launches=s["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 avg_flop_per_launch=s["flops"] / s["launches"],
                 timing="hip events bound to the kernel dispatch (hipExtLaunchKernelGGL), "

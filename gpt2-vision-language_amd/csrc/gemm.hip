@@ -333,8 +333,12 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
 // (9-36 tiles of 256x256 at K = 16384 tokens) to fill the chip without a K split and fp32
 // slabs, together they do.  Epilogue: plain or C += AB (residual == c, fused accumulation);
 // anything else, or an unsupported shape, runs the problems one by one through gvl_gemm.
+// name of the kernel instance the last batched call launched ("" after a per-problem fallback)
+static thread_local char g_batched_name[128];
+
 static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
                              gvl_stream_t stream) {
+  g_batched_name[0] = 0;
   GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_batched: bad arguments");
   bool ok = count > 1 && count <= GVL_MAX_BATCH && env().impl >= 3 && env().cfg < 0;
   // fused bias gradients: weight-gradient layout (both operands MN-contiguous), C += AB
@@ -434,6 +438,11 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
     }
     return 0;
   }
+  {
+    const char* tf[2] = {"false", "true"};
+    snprintf(g_batched_name, sizeof g_batched_name, "gemm_pp3_kernel<4, %s, %s, %d, %d, %d>",
+             tf[d[0].a_mn != 0], tf[d[0].b_mn != 0], gvl::gemm_epi_kind(p), p.bn, p.bm);
+  }
   gvl::gemm_pp3_launch(p, d[0].a_mn, d[0].b_mn, gvl::as_stream(stream));
   GVL_LAUNCH_CHECK("gvl_gemm_batched");
   if (dbias && p.splits == 2) {  // dbias[i] += column sums of dY_i = A_i stored [K][M]
@@ -448,6 +457,12 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
 
 extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream) {
   return gemm_batched_impl(d, nullptr, count, stream);
+}
+
+extern "C" int gvl_gemm_batched_kernel_name(char* buf, int32_t len) {
+  GVL_REQUIRE(buf && len > 0, "gvl_gemm_batched_kernel_name: bad arguments");
+  snprintf(buf, len, "%s", g_batched_name);
+  return 0;
 }
 
 extern "C" int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t count,

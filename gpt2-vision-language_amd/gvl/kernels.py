@@ -251,17 +251,35 @@ def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
         if tk is not None:  # the library may split a batch that underfills the chip in two
             d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
-    if dbias is not None:
-        for t in dbias:
-            if t.dtype != BF16 or not t.is_contiguous():
-                raise ValueError("gvl.gemm_batched: dbias must be contiguous bf16")
-        da = (C.c_void_p * n)(*[t.data_ptr() for t in dbias])
-        rc = _L().gvl_gemm_batched_dbias(arr, da, n, _stream())
-        if rc not in (0, -1):  # -1: nothing launched, the caller runs the unfused pair
-            _lib.check(rc, "gvl_gemm_batched_dbias")
-        return rc == 0
-    _lib.check(_L().gvl_gemm_batched(arr, n, _stream()), "gvl_gemm_batched")
-    return True
+    ev = None
+    if _timer is not None and _timer.dispatch:  # bound to the batched kernel's own dispatch
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        ev[1].record()
+        _L().gvl_set_launch_events(C.c_void_p(ev[0].cuda_event), C.c_void_p(ev[1].cuda_event))
+    try:
+        if dbias is not None:
+            for t in dbias:
+                if t.dtype != BF16 or not t.is_contiguous():
+                    raise ValueError("gvl.gemm_batched: dbias must be contiguous bf16")
+            da = (C.c_void_p * n)(*[t.data_ptr() for t in dbias])
+            rc = _L().gvl_gemm_batched_dbias(arr, da, n, _stream())
+            if rc not in (0, -1):  # -1: nothing launched, the caller runs the unfused pair
+                _lib.check(rc, "gvl_gemm_batched_dbias")
+            ok = rc == 0
+        else:
+            _lib.check(_L().gvl_gemm_batched(arr, n, _stream()), "gvl_gemm_batched")
+            ok = True
+    finally:
+        if ev is not None:
+            _L().gvl_set_launch_events(None, None)
+    if ev is not None and ok:
+        buf = C.create_string_buffer(128)
+        _L().gvl_gemm_batched_kernel_name(buf, 128)
+        if buf.value:  # one batched launch (not the per-problem fallback)
+            flops = sum(2.0 * arr[i].m * arr[i].n * arr[i].k for i in range(n))
+            _timer.records.append((buf.value.decode(), ev[0], ev[1], flops))
+    return ok
 
 
 # ------------------------------------------------------------------------- LayerNorm

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 6
+#define GVL_ABI_VERSION 7
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -118,6 +118,10 @@ int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
  * caller attribute event timings to the rocprofv3 kernel-trace rows). */
 int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len);
+/* ABI v7: name of the kernel instance the calling thread's last gvl_gemm_batched /
+ * gvl_gemm_batched_dbias call launched as one batched launch ("" when it ran the problems one
+ * by one through gvl_gemm): the bench attributes the batched weight-gradient launches too. */
+int gvl_gemm_batched_kernel_name(char* buf, int32_t len);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (eps given; reference uses 1e-5).

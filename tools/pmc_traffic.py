@@ -25,8 +25,9 @@ def short(name):
     return m.group(0) if m else s.split("(")[0][:120]
 
 
-def load(d, counter):
-    acc = defaultdict(lambda: [0.0, 0])
+def load(d, counter, with_time=False):
+    """kernel -> [sum of the counter over dispatches, dispatches(, sum of durations in ns)]"""
+    acc = defaultdict(lambda: [0.0, 0, 0.0])
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
@@ -35,16 +36,41 @@ def load(d, counter):
                 k = short(row["Kernel_Name"])
                 acc[k][0] += float(row["Counter_Value"])
                 acc[k][1] += 1
+                acc[k][2] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
     return acc
+
+
+CUS, SIMDS = 256, 4
+
+
+def mfma_clock(root, wl):
+    """kernel -> (MFMA busy fraction, achieved clock in GHz).  SQ_VALU_MFMA_BUSY_CYCLES sums the
+    matrix-pipe cycles over every SIMD (16 per 16x16x32 bf16 MFMA: 2^30 for an 8192^3 GEMM,
+    profiles/r1/pmc), GRBM_GUI_ACTIVE the GPU-busy cycles over the 8 XCDs (MI355X_MICROARCH.md
+    'DVFS give-back'), so busy = MFMA / (CUs x SIMDs x GRBM / 8) and clock = GRBM / 8 / duration.
+    busy x clock / 2.4 GHz = the fraction of the 2.4 GHz bf16 peak the kernel reached."""
+    d = os.path.join(root, f"{wl}_SQ_VALU_MFMA_BUSY_CYCLES")
+    mf = load(d, "SQ_VALU_MFMA_BUSY_CYCLES")
+    gr = load(d, "GRBM_GUI_ACTIVE")
+    out = {}
+    for k, (m, n, _) in mf.items():
+        if k not in gr or not n or not gr[k][1] or gr[k][0] <= 0 or gr[k][2] <= 0:
+            continue
+        cyc = gr[k][0] / 8.0
+        out[k] = (m / (CUS * SIMDS * cyc), cyc / gr[k][2])
+    return out
 
 
 def main(root):
     out = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                     "eager bench steps; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch",
+                     "eager bench steps; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch; "
+                     "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), "
+                     "clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel duration (third pass)",
            "workloads": {}}
     for wl in ("lm", "qf"):
         fe = load(os.path.join(root, f"{wl}_FETCH_SIZE"), "FETCH_SIZE")
         wr = load(os.path.join(root, f"{wl}_WRITE_SIZE"), "WRITE_SIZE")
+        mc = mfma_clock(root, wl)
         ks = {}
         for k in fe:
             if k not in wr or not fe[k][1] or not wr[k][1]:
@@ -52,6 +78,9 @@ def main(root):
             f_kib, w_kib = fe[k][0] / fe[k][1], wr[k][0] / wr[k][1]
             ks[k] = dict(launches=fe[k][1], fetch_kib=round(f_kib, 1), write_kib=round(w_kib, 1),
                          hbm_bytes=round(2 * f_kib * 1024 + w_kib * 1024))
+            if k in mc:
+                ks[k]["mfma_busy"] = round(mc[k][0], 4)
+                ks[k]["clock_ghz"] = round(mc[k][1], 3)
         out["workloads"][wl] = dict(sorted(ks.items(), key=lambda kv: -kv[1]["hbm_bytes"] * kv[1]["launches"]))
     print(json.dumps(out, indent=1))
 

@@ -9,10 +9,12 @@ OUT=gpurun_out/pmc_traffic_$TAG; mkdir -p $OUT
 # Round 1 ran these passes with AMD_SERIALIZE_KERNEL=3 after one HSA_STATUS_ERROR_INVALID_PACKET_FORMAT
 # abort; the same eager LM pass without it completed in round 2 (tools/pmc_calib.sh,
 # profiles/r2/pmc_calibration.md), so the passes run unserialised.
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/lm_$c -o run -- \
-    python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $OUT/lm_$c.log 2>&1 || exit $?
-  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/qf_$c -o run -- \
-    python bench.py --workload qformer --steps 2 --warmup 0 --no-cpu-baseline --no-graph > $OUT/qf_$c.log 2>&1 || exit $?
+# Third pass: MFMA busy cycles + achieved clock (SQ 2 + GRBM 1 counters: one pass).
+for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  d=${c%% *}
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/lm_$d -o run -- \
+    python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $OUT/lm_$d.log 2>&1 || exit $?
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/qf_$d -o run -- \
+    python bench.py --workload qformer --steps 2 --warmup 0 --no-cpu-baseline --no-graph > $OUT/qf_$d.log 2>&1 || exit $?
 done
 python tools/pmc_traffic.py $OUT > gpurun_out/pmc_traffic_$TAG.json
