@@ -24,15 +24,21 @@ def test_kernel_name_shortening_matches_bench_names():
 def test_traffic_table_from_counter_csvs(tmp_path):
     T = _load("pmc_traffic", os.path.join(ROOT, "tools", "pmc_traffic.py"))
     name = "void (anonymous namespace)::gemm_pp3_kernel<4, false, true, 0>(GemmP)"
+    # third pass: MFMA busy cycles + GRBM_GUI_ACTIVE in one directory, 10 us dispatches
+    passes = (("FETCH_SIZE", "FETCH_SIZE", [100.0, 300.0]), ("WRITE_SIZE", "WRITE_SIZE", [50.0, 50.0]),
+              ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", [1024 * 8000.0, 1024 * 8000.0]),
+              ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", [8 * 20000.0, 8 * 20000.0]))
     for wl in ("lm", "qf"):
-        for ctr, vals in (("FETCH_SIZE", [100.0, 300.0]), ("WRITE_SIZE", [50.0, 50.0])):
-            d = tmp_path / f"{wl}_{ctr}" / "host"
+        for i, (dname, ctr, vals) in enumerate(passes):
+            d = tmp_path / f"{wl}_{dname}" / f"host{i}"
             d.mkdir(parents=True)
             with open(d / "run_counter_collection.csv", "w", newline="") as f:
-                w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+                w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value",
+                                                  "Start_Timestamp", "End_Timestamp"])
                 w.writeheader()
                 for v in vals:
-                    w.writerow(dict(Kernel_Name=name, Counter_Name=ctr, Counter_Value=v))
+                    w.writerow(dict(Kernel_Name=name, Counter_Name=ctr, Counter_Value=v,
+                                    Start_Timestamp=1000, End_Timestamp=11000))
     import contextlib
     import io
     buf = io.StringIO()
@@ -42,6 +48,8 @@ def test_traffic_table_from_counter_csvs(tmp_path):
     k = out["workloads"]["lm"]["gemm_pp3_kernel<4, false, true, 0>"]
     # FETCH_SIZE doubled (gfx950 streaming-read correction), both counters in KiB
     assert k["launches"] == 2 and k["hbm_bytes"] == round(2 * 200.0 * 1024 + 50.0 * 1024)
+    # 8000 busy cycles per SIMD over 20000 cycles per XCD; 20000 cycles in 10 us = 2 GHz
+    assert k["mfma_busy"] == 0.4 and k["clock_ghz"] == 2.0
 
 
 def test_committed_traffic_covers_bench_dominant_kernels():

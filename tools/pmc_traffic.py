@@ -36,7 +36,8 @@ def load(d, counter, with_time=False):
                 k = short(row["Kernel_Name"])
                 acc[k][0] += float(row["Counter_Value"])
                 acc[k][1] += 1
-                acc[k][2] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                if row.get("End_Timestamp") and row.get("Start_Timestamp"):
+                    acc[k][2] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
     return acc
 
 
