@@ -375,17 +375,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
 // the fragment reads).
 constexpr int DK_SLOT = 2 * KT * D * 2 + 2 * KT * 4;  // Q, dO tiles + lse2, D rows
 
-// Transposed fragment reads of the LDS-DMA backward kernels.
-// dK/dV kernel: inline asm without a wait, then one lgkmcnt(0) asm naming the fragments
-// (lds_wait8): with the DMA issued through the builtin, hipcc treats a ds_read_b64_tr_b16
-// builtin as possibly aliasing the in-flight LDS write and drains vmcnt(0) in front of it; the
-// builtin form below also spills this kernel (168-VGPR budget at 3 waves per SIMD).  The form
-// is fragile — an asm VGPR destination counts as written at ;;#ASMEND, so hipcc may copy it
-// before the wait; the shipped ISA copies in-flight destinations only into registers nothing
-// reads (checked with tools/asm_hazards.py).
-// dQ kernel: the DMA is inline asm (gvl_ring::dma16_lds), so hipcc sees no pending LDS write and the
-// builtin transposed read needs no vmcnt; its lgkmcnt waits are hipcc's own (no asm
-// destinations at all).
+// frag_tr<false> by inline asm, without a wait: hipcc treats a ds_read_b64_tr_b16 builtin as
+// possibly aliasing any in-flight LDS DMA and drains vmcnt(0) in front of it.  The caller
+// waits (lds_wait8) before the MFMAs use the fragments.
 GVL_DEV short8_t frag_tr_asm(const char* lds, int t, int s, int lane) {
   const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int ch = 2 * t + (p >> 1);
@@ -407,15 +399,6 @@ GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
                  "+v"(b[3])
                :
                : "memory");
-}
-GVL_DEV short8_t frag_tr_b(const char* lds, int t, int s, int lane) {
-  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int ch = 2 * t + (p >> 1);
-  const int ra = 32 * s + 4 * G + q, rb = ra + 16;
-  short8_t r;
-  r.lo = lds_read_tr(lds + swz_tr(ra, ch) + (p & 1) * 8);
-  r.hi = lds_read_tr(lds + swz_tr(rb, ch) + (p & 1) * 8);
-  return r;
 }
 
 // G key groups of 16 per wave (64 G keys per block): every Q / dO fragment read from LDS
@@ -670,8 +653,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
       const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
       const int vok = (int)(((k0 + row) * p.k_st + chunk * 8) * 2);
       const int vov = (int)(((k0 + row) * p.v_st + chunk * 8) * 2);
-      gvl_ring::dma16_lds(rk, vok, 0, sb + j * 1024);  // inline asm: see frag_tr_b
-      gvl_ring::dma16_lds(rv, vov, 0, sb + KT * D * 2 + j * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void_t*)(sb + j * 1024), 16, vok, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void_t*)(sb + KT * D * 2 + j * 1024), 16,
+                                               vov, 0, 0, 0);
     }
   };
   if (nkt > 0) {
@@ -728,9 +712,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      short8_t kt4[4];
+      short8_t kt4[4], kt4b[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) kt4[t] = frag_tr_b(ks, t, s2, lane);
+      for (int t = 0; t < 4; ++t) kt4[t] = frag_tr_asm(ks, t, s2, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kt4b[t] = kt4[t];
+      lds_wait8(kt4, kt4b);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
