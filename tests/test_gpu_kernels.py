@@ -158,63 +158,6 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
-@pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d", "mul", "bias_res",
-                                 "res_inplace_bias"])
-@pytest.mark.parametrize("M,N,K", [(8064, 3072, 768), (7999, 2240, 768), (16384, 768, 3072),
-                                   (4096, 2304, 768)])
-def test_gemm_deferred_epilogue(cuda, epi, M, N, K):
-    """Deferred epilogue of the persistent kernel (gemm_pp3.h DefEpi, 256 x 192 tiles): the
-    tile's outputs are rounded to bf16 at the tile boundary (acc + bias, as the reference's
-    autocast nn.Linear output) and finished one fragment per K-step of the next tile with
-    dropped out-of-range stores.  Every kind, ragged M and N (M-tail rows, a partial last
-    column tile), several tiles per CU, the in-place residual; vs the reference semantics
-    (GELU / gelu' / the gelu' product / the residual add applied to the bf16-rounded branch)."""
-    K_ = _k()
-    torch.manual_seed(M + N + K + len(epi))
-    mul = epi == "mul"
-    a = torch.randn(M, K).to(BF)
-    b = (torch.randn(K, N) * 0.05).to(BF)
-    A = a.to(cuda)
-    B = (b if mul else b.t().contiguous()).to(cuda)
-    name = _kernel_name(A, B, 0, int(mul), M, N, K, epi={"bias_act_erf_d": "bias_act_d",
-                                                        "res_inplace_bias": "bias_res"}.get(epi, epi))
-    assert name.endswith(", 192, 256, true>"), name
-    h = a.float() @ b.float()
-    bias = torch.randn(N).to(BF)
-    aux = torch.randn(M, N).to(BF)
-    hb = (h + (0 if epi in ("plain", "mul") else bias.float())).to(BF).float()  # bf16 branch
-    kw = {}
-    if epi == "plain":
-        ref = hb
-    elif epi == "bias":
-        kw, ref = dict(bias=bias.to(cuda)), hb
-    elif epi in ("bias_act_d", "bias_act_erf_d"):
-        erf = epi == "bias_act_erf_d"
-        x = hb.clone().requires_grad_(True)
-        g = O.gelu_erf(x) if erf else O.gelu_tanh(x)
-        g.sum().backward()
-        pre = torch.empty(M, N, dtype=BF, device=cuda)
-        kw, ref = dict(bias=bias.to(cuda), act=4 if erf else 3, pre_out=pre), g.detach()
-    elif mul:
-        kw, ref = dict(dact=3, pre_in=aux.to(cuda)), hb * aux.float()
-    else:  # bias + residual, out of place or in place (out is the residual)
-        r = aux.to(cuda)
-        kw = dict(bias=bias.to(cuda), residual=r)
-        if epi == "res_inplace_bias":
-            kw["out"] = r
-        ref = hb + aux.float()
-    y = K_.gemm(A, B, b_mn=mul, **kw)
-    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
-    if epi in ("bias_act_d", "bias_act_erf_d"):
-        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
-    # an M-tail / N-tail store must not land outside the output: a second call into a
-    # sentinel-bordered buffer leaves the border untouched
-    if epi == "bias" and (M % 256 or N % 192):
-        big = torch.full((M + 3, N + 64), 7.0, dtype=BF, device=cuda)
-        K_.gemm(A, B, out=big[:M, :N], **kw)
-        assert torch.all(big[M:] == 7.0) and torch.all(big[:, N:] == 7.0)
-
-
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("epi", ["plain", "bias_res", "res_inplace", "bias_act", "dact"])
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (12000, 1536, 320), (16384, 2304, 32)])
@@ -274,7 +217,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
         name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
     finally:
         _lib.lib().gvl_gemm_tune(3, -1)
-    assert name.startswith("gemm_pp3_kernel") and ", 192, 256, " in name, name
+    assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 256>"), name
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
@@ -334,7 +277,7 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
     if not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
         assert name.startswith(_w4_name(M, K, epi)), name
     else:
-        assert name.startswith("gemm_pp3_kernel") and ", 192, 128, " in name, name
+        assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)

@@ -25,7 +25,7 @@ r4a)  # HEAD check + epilogue share of the short-K wide GEMMs (timing-only pp3 b
   for v in pp3d1 pp3d2 base; do diag $v 8064 wide epi; diag $v 16384 wide epi; done
   ;;
 r4b)  # deferred epilogue + asm LDS-DMA: GEMM kernel tests, then A/B shapes and the two steps
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "gemm or batched or deferred" --timeout 300 \
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "gemm or batched" --timeout 300 \
     --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
   diag dmab 8064 all epi; diag base 8064 all all; GVL_PP3_DEFER=0 diag base 8064 wide epi
   diag dmab 16384 wide epi; diag base 16384 wide epi
