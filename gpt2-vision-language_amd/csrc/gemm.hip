@@ -207,7 +207,6 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.drop_scale = p.has_drop ? 1.f / (1.f - d->drop_p) : 1.f;
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
-  p.a_mn = d->a_mn != 0; p.b_mn = d->b_mn != 0;
   p.splits = 1;
   p.bn = 256;
   p.bm = 256;
@@ -250,7 +249,7 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
-               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm, tf[gvl::gemm_pp3_defer(p)]);
+               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm, tf[gvl::gemm_pp3_defer(p, d->a_mn != 0, d->b_mn != 0)]);
     } else {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn)),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);

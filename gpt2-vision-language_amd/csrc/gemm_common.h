@@ -28,7 +28,6 @@ struct GemmP {
   int bm;     // output tile height of the persistent kernel (256, or 128 with bn 192)
   int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
-  int a_mn, b_mn;  // operand layouts (the call's descriptor)
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
   // writing fp32 partials to ws[s][M][N]; gemm_splitk_reduce applies the epilogue.
   int splits;
@@ -491,7 +490,7 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
 // planned p runs on a deferred-epilogue instance of gemm_pp3_kernel (gemm_pp3.h DefEpi)
-bool gemm_pp3_defer(const GemmP& p);
+bool gemm_pp3_defer(const GemmP& p, bool a_mn, bool b_mn);
 int gemm_pp3_launch_ff(const GemmP& p, hipStream_t s);  // gemm_pp3_{ff,ft,tf,tt}.hip
 int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);
 int gemm_pp3_launch_tf(const GemmP& p, hipStream_t s);

@@ -114,9 +114,7 @@ static void pp3_choose_combined(GemmP& p, int gran) {
   p.kper = p.K / p.splits;
 }
 
-// epilogue kind + operand layout pairs with deferred-epilogue instances (gemm_pp3.h DefEpi:
-// forward outputs with B = the [N, K] weight, and the MLP's dX x gelu'(x)); GVL_PP3_DEFER=0:
-// none
+// epilogue kinds with deferred-epilogue instances (GVL_PP3_DEFER=0: none)
 static bool pp3_defer_on() {
   static const bool on = [] {
     const char* e = getenv("GVL_PP3_DEFER");
@@ -126,10 +124,8 @@ static bool pp3_defer_on() {
 }
 static bool pp3_defer_kind(const GemmP& p) {
   const int epi = gemm_epi_kind(p);
-  if (!pp3_defer_on() || p.a_mn) return false;
-  if (epi == EPI_MUL) return p.b_mn;
-  return !p.b_mn && (epi == EPI_PLAIN || epi == EPI_BIAS || epi == EPI_BIAS_ACT_D ||
-                     epi == EPI_BIAS_ACT_ERF_D || epi == EPI_BIAS_RES);
+  return pp3_defer_on() && (epi == EPI_BIAS || epi == EPI_BIAS_ACT_D || epi == EPI_BIAS_ACT_ERF_D ||
+                            epi == EPI_MUL);
 }
 
 // Tile height 128 (with 192-wide tiles) when its tiles fill the CUs in fewer rounds than the
@@ -202,20 +198,18 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
 // on 256 x 192 tiles, one problem, no K split, at least one 32-deep K-step per pending
 // fragment (24), 32-bit store offsets below the dropped-store offset, a 16-B aligned bias row
 // that fits in LDS beside the ring.  GVL_PP3_DEFER=0 keeps the in-place epilogue (A/B).
-bool gemm_pp3_defer(const GemmP& p) {
-  if (!pp3_defer_kind(p)) return false;
+bool gemm_pp3_defer(const GemmP& p, bool a_mn, bool b_mn) {
+  const bool on = pp3_defer_on();
   const int epi = gemm_epi_kind(p);
   const bool act = epi == EPI_BIAS_ACT_D || epi == EPI_BIAS_ACT_ERF_D, mul = epi == EPI_MUL;
-  const bool res = epi == EPI_BIAS_RES, bias = epi != EPI_PLAIN && !mul;
+  if (!on || a_mn || !(epi == EPI_BIAS || act || mul) || b_mn != mul) return false;
   constexpr int64_t OOB = 0x7FFFFFF0;  // gemm_pp3.h DEF_OOB
-  const int64_t lds = 4 * (256 + 192) * KS * 2 + (bias ? 2 * (int64_t)p.tiles_n * 192 : 0) +
-                      (mul || res ? 8 * 512 : 0);
-  const bool bias_ok = !bias || (p.bias != nullptr && (reinterpret_cast<uintptr_t>(p.bias) & 15) == 0);
+  const int64_t lds = 4 * (256 + 192) * KS * 2 + 2 * (int64_t)p.tiles_n * 192 + 8 * 512;
+  const bool bias_ok = mul || (p.bias != nullptr && (reinterpret_cast<uintptr_t>(p.bias) & 15) == 0);
   return p.bm == 256 && p.bn == 192 && p.splits == 1 && p.batch == 1 && p.kper / KS >= 24 &&
          bias_ok && lds <= 160 * 1024 && p.M * p.ldc * 2 <= OOB &&
          (!act || (p.pre_out != nullptr && p.M * p.ldp * 2 <= OOB)) &&
-         (!mul || (p.pre_in != nullptr && p.M * p.ldp * 2 <= OOB)) &&
-         (!res || (p.residual != nullptr && p.M * p.ldr * 2 <= OOB));
+         (!mul || (p.pre_in != nullptr && p.M * p.ldp * 2 <= OOB));
 }
 
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s) {

@@ -55,13 +55,11 @@ constexpr uint32_t DEF_OOB = 0x7FFFFFF0u;  // voffset past any buffer: the acces
 template <int EPI, int FM, int FN>
 struct DefEpi {
   using KD = EpiKind<EPI>;
-  static constexpr bool ON = EPI == EPI_PLAIN || EPI == EPI_BIAS || EPI == EPI_BIAS_ACT_D ||
-                             EPI == EPI_BIAS_ACT_ERF_D || EPI == EPI_MUL || EPI == EPI_BIAS_RES;
-  static constexpr bool RES = EPI == EPI_BIAS_RES;
+  static constexpr bool ON = EPI == EPI_BIAS || EPI == EPI_BIAS_ACT_D || EPI == EPI_BIAS_ACT_ERF_D ||
+                             EPI == EPI_MUL;
   static constexpr int NCH = FM * FN;         // one fragment per chunk
   static constexpr int ES = KD::ACT ? 2 : 1;  // stores per chunk: output (+ gelu'(x))
-  // the next chunk's [M, N] operand (gelu'(x) for MUL, the residual for BIAS_RES): 2 DMA pieces
-  static constexpr int EL = KD::MUL || RES ? 2 : 0;
+  static constexpr int EL = KD::MUL ? 2 : 0;  // the next chunk's gelu'(x) operand (MUL): 2 DMA
   static constexpr int EOPS = ES + EL;        // VMEM ops every M phase issues
   typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
@@ -92,11 +90,6 @@ struct DefEpi {
           u32x2_t{pack2(lo_bf(w0) * lo_bf(aux[0]), hi_bf(w0) * hi_bf(aux[0])),
                   pack2(lo_bf(w1) * lo_bf(aux[1]), hi_bf(w1) * hi_bf(aux[1]))},
           rc, oc, 0, 0);
-    } else if constexpr (RES) {  // x + bf16(x W^T + b): the residual add of the bf16 branch
-      __builtin_amdgcn_raw_buffer_store_b64(
-          u32x2_t{pack2(lo_bf(w0) + lo_bf(aux[0]), hi_bf(w0) + hi_bf(aux[0])),
-                  pack2(lo_bf(w1) + lo_bf(aux[1]), hi_bf(w1) + hi_bf(aux[1]))},
-          rc, oc, 0, 0);
     } else {
       __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{w0, w1}, rc, oc, 0, 0);
     }
@@ -118,8 +111,7 @@ struct DefEpi {
         __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pend[0][0][0], pend[0][0][1]}, rc, DEF_OOB, 0, 0);
     }
   }
-  // MUL / BIAS_RES: the [M, N] operand (leading dimension ld) of chunk q of the tile at wave
-  // origin (m0, n0) (q >= NCH or
+  // MUL: the gelu'(x) operand of chunk q of the tile at wave origin (m0, n0) (q >= NCH or
   // !valid: dropped loads) into this wave's 512-B LDS slot by two 4-B-per-lane LDS-DMA pieces
   // (no VGPR destination: nothing hipcc could copy before the data lands; counted by the
   // ring's waits like the K-step pieces); aux_read() retires and reads it.
@@ -128,8 +120,7 @@ struct DefEpi {
     const int i = q / FN, j = q - (q / FN) * FN;
     const int64_t m = m0 + 16 * i + (lane & 15), n = n0 + 16 * j + 4 * (lane >> 4);
     const bool ok = valid && q < NCH && m < p.M && n < p.N;
-    const int64_t ld = RES ? p.ldr : p.ldp;
-    const int off = (int)(ok ? (uint32_t)((m * ld + n) * 2) : DEF_OOB);
+    const int off = (int)(ok ? (uint32_t)((m * p.ldp + n) * 2) : DEF_OOB);
     dma4_lds(ra, off, 0, aux_lds);
     dma4_lds(ra, off + 4, 0, aux_lds + 256);
   }
@@ -300,12 +291,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   typename DE::u32x2_t paux = {0u, 0u};  // MUL: gelu'(x) of chunk pq
   const char* bias_lds = smem + NS * SLOT;
   // MUL: per-wave 512-B slot for the next chunk's gelu'(x), after the bias row
-  const char* aux_lds = smem + NS * SLOT + (EpiKind<EPI>::BIAS ? 2 * p.tiles_n * BN : 0) + wave * 512;
+  const char* aux_lds = smem + NS * SLOT + 2 * p.tiles_n * BN + wave * 512;
   // (DEF) output / gelu' buffers; non-DEF instances never read them
   const __amdgpu_buffer_rsrc_t rc_def = uniform_rsrc(p.C, DEF ? p.M * p.ldc * 2 : 0);
   const __amdgpu_buffer_rsrc_t rp_def = uniform_rsrc(
-      EpiKind<EPI>::ACT ? p.pre_out : EpiKind<EPI>::MUL ? p.pre_in : DE::RES ? p.residual : p.C,
-      DEF ? p.M * (EpiKind<EPI>::ACT || EpiKind<EPI>::MUL ? p.ldp : DE::RES ? p.ldr : p.ldc) * 2 : 0);
+      EpiKind<EPI>::ACT ? p.pre_out : EpiKind<EPI>::MUL ? p.pre_in : p.C,
+      DEF ? p.M * (EpiKind<EPI>::ACT || EpiKind<EPI>::MUL ? p.ldp : p.ldc) * 2 : 0);
   if constexpr (DEF) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -482,7 +473,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
         for (int q = 1; q < DE::NCH; ++q) {
           const int64_t m = cu_m0 + arow + 16 * (q / FN) + (lane & 15);
           const int64_t n = cu_n0 + bcol + 16 * (q % FN) + 4 * (lane >> 4);
-          const uint32_t off = (m < p.M && n < p.N) ? (uint32_t)((m * (DE::RES ? p.ldr : p.ldp) + n) * 2) : DEF_OOB;
+          const uint32_t off = (m < p.M && n < p.N) ? (uint32_t)((m * p.ldp + n) * 2) : DEF_OOB;
           ax[q] = __builtin_bit_cast(typename DE::u32x2_t,
                                      __builtin_amdgcn_raw_buffer_load_b64(rp_def, off, 0, 0));
         }
@@ -501,10 +492,7 @@ template <int NS, bool AMN, bool BMN, int EPI, int BN, int BM, bool DEFER = fals
 int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
   GemmP p = p0;  // tiles_m/n, splits, kper set by gemm_pp3_try
   // DEFER: the bias row's LDS copy follows the ring
-  // DEFER: bias row (bias kinds), then 8 x 512 B of next-chunk operands (MUL / BIAS_RES)
-  using DE = DefEpi<EPI, BM / 32, BN / 64>;
-  const int lds = NS * (BM + BN) * KS * 2 +
-                  (DEFER ? (EpiKind<EPI>::BIAS ? 2 * p.tiles_n * BN : 0) + (DE::EL ? 8 * 512 : 0) : 0);
+  const int lds = NS * (BM + BN) * KS * 2 + (DEFER ? 2 * p.tiles_n * BN + 8 * 512 : 0);
   auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI, BN, BM, DEFER>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -533,8 +521,8 @@ template <int NS, bool AMN, bool BMN, int EPI>
 int launch_pp3(const GemmP& p, hipStream_t s) {
   if (p.bm == 128) return launch_pp3_bn<GVL_PP3_NS_128, AMN, BMN, EPI, 192, 128>(p, s);
   // deferred-epilogue instances: forward outputs (B = the [N, K] weight) and the MLP's dX x gelu'
-  if constexpr (DefEpi<EPI, 8, 3>::ON && !AMN && BMN == (EPI == EPI_MUL)) {
-    if (gvl::gemm_pp3_defer(p)) return launch_pp3_bn<GVL_PP3_NS_192, AMN, BMN, EPI, 192, 256, true>(p, s);
+  if constexpr (!AMN && DefEpi<EPI, 8, 3>::ON && (BMN == (EPI == EPI_MUL))) {
+    if (gvl::gemm_pp3_defer(p, AMN, BMN)) return launch_pp3_bn<GVL_PP3_NS_192, AMN, BMN, EPI, 192, 256, true>(p, s);
   }
   return p.bn == 192 ? launch_pp3_bn<GVL_PP3_NS_192, AMN, BMN, EPI, 192, 256>(p, s)
                      : launch_pp3_bn<GVL_PP3_NS_256, AMN, BMN, EPI, 256, 256>(p, s);
