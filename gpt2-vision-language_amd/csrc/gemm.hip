@@ -248,8 +248,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     } else if (gvl::gemm_pp3_plan(p, cfg == 3 || cfg == 10)) {
       const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
-      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d, %s>", tf[d->a_mn != 0], tf[d->b_mn != 0],
-               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm, tf[gvl::gemm_pp3_defer(p, d->a_mn != 0, d->b_mn != 0)]);
+      snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
+               epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm);
     } else {
       snprintf(buf, len, "%s, %s, %s>", gvl::gemm_ring_name(gvl::gemm_ring_pick(d->m, d->n, d->k, -1, d->a_mn)),
                tf[d->a_mn != 0], tf[d->b_mn != 0]);
@@ -440,7 +440,7 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
   }
   {
     const char* tf[2] = {"false", "true"};
-    snprintf(g_batched_name, sizeof g_batched_name, "gemm_pp3_kernel<4, %s, %s, %d, %d, %d, false>",
+    snprintf(g_batched_name, sizeof g_batched_name, "gemm_pp3_kernel<4, %s, %s, %d, %d, %d>",
              tf[d[0].a_mn != 0], tf[d[0].b_mn != 0], gvl::gemm_epi_kind(p), p.bn, p.bm);
   }
   gvl::gemm_pp3_launch(p, d[0].a_mn, d[0].b_mn, gvl::as_stream(stream));

@@ -489,8 +489,6 @@ int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels (gemm_pl
 bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
-// planned p runs on a deferred-epilogue instance of gemm_pp3_kernel (gemm_pp3.h DefEpi)
-bool gemm_pp3_defer(const GemmP& p, bool a_mn, bool b_mn);
 int gemm_pp3_launch_ff(const GemmP& p, hipStream_t s);  // gemm_pp3_{ff,ft,tf,tt}.hip
 int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);
 int gemm_pp3_launch_tf(const GemmP& p, hipStream_t s);

@@ -114,20 +114,6 @@ static void pp3_choose_combined(GemmP& p, int gran) {
   p.kper = p.K / p.splits;
 }
 
-// epilogue kinds with deferred-epilogue instances (GVL_PP3_DEFER=0: none)
-static bool pp3_defer_on() {
-  static const bool on = [] {
-    const char* e = getenv("GVL_PP3_DEFER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static bool pp3_defer_kind(const GemmP& p) {
-  const int epi = gemm_epi_kind(p);
-  return pp3_defer_on() && (epi == EPI_BIAS || epi == EPI_BIAS_ACT_D || epi == EPI_BIAS_ACT_ERF_D ||
-                            epi == EPI_MUL);
-}
-
 // Tile height 128 (with 192-wide tiles) when its tiles fill the CUs in fewer rounds than the
 // 256-row tiles: estimated per-tile cost 0.375 / E128 of a 256x256 tile (E128 = per-FLOP
 // efficiency of the half-height tile, GVL_PP3_E128 x 100, default 70: measured equal to the
@@ -174,12 +160,6 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   if (p.splits == 1 && gemm_epi_kind(p) == EPI_GEN) return false;
   p.bn = 256;
   if (p.splits == 1 && gran == KS) p.bn = pp3_tile_width(p.M, p.N);
-  // the deferred-epilogue instances are 256 x 192 (gemm_pp3.h DefEpi): their kinds take
-  // 192-wide tiles wherever those fit the K-step ring, since the hidden epilogue outweighs the
-  // wider tile's fill advantage (M = 16384: c_fc / mlp.c_proj dX at 768 tiles of 256 x 256)
-  if (p.splits == 1 && gran == KS && p.bn == 256 && p.N % 64 == 0 && p.N >= 384 &&
-      pp3_defer_kind(p) && p.K / KS >= 24)
-    p.bn = 192;
   if (p.splits == 1 && gran == KS && pp3_tile_height(p.M, p.N, p.bn) == 128) {
     p.bm = 128;
     p.bn = 192;
@@ -192,24 +172,6 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   // >= 64 tiles the 128x128 ring at two workgroups per CU is faster
   if (p.splits > 1 && tiles >= 64) return false;
   return tiles * p.splits >= pp3_min_items();
-}
-
-// Deferred-epilogue routing (gemm_pp3.h, DefEpi): plain-bias and bias + GELU(-deriv) outputs
-// on 256 x 192 tiles, one problem, no K split, at least one 32-deep K-step per pending
-// fragment (24), 32-bit store offsets below the dropped-store offset, a 16-B aligned bias row
-// that fits in LDS beside the ring.  GVL_PP3_DEFER=0 keeps the in-place epilogue (A/B).
-bool gemm_pp3_defer(const GemmP& p, bool a_mn, bool b_mn) {
-  const bool on = pp3_defer_on();
-  const int epi = gemm_epi_kind(p);
-  const bool act = epi == EPI_BIAS_ACT_D || epi == EPI_BIAS_ACT_ERF_D, mul = epi == EPI_MUL;
-  if (!on || a_mn || !(epi == EPI_BIAS || act || mul) || b_mn != mul) return false;
-  constexpr int64_t OOB = 0x7FFFFFF0;  // gemm_pp3.h DEF_OOB
-  const int64_t lds = 4 * (256 + 192) * KS * 2 + 2 * (int64_t)p.tiles_n * 192 + 8 * 512;
-  const bool bias_ok = mul || (p.bias != nullptr && (reinterpret_cast<uintptr_t>(p.bias) & 15) == 0);
-  return p.bm == 256 && p.bn == 192 && p.splits == 1 && p.batch == 1 && p.kper / KS >= 24 &&
-         bias_ok && lds <= 160 * 1024 && p.M * p.ldc * 2 <= OOB &&
-         (!act || (p.pre_out != nullptr && p.M * p.ldp * 2 <= OOB)) &&
-         (!mul || (p.pre_in != nullptr && p.M * p.ldp * 2 <= OOB));
 }
 
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s) {

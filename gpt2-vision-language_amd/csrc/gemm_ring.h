@@ -20,45 +20,6 @@ GVL_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
       reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-// One 1-KiB LDS-DMA piece (buffer_load_dwordx4 ... lds: 64 lanes x 16 B to lds + 16 lane) as
-// inline asm.  Issued through the builtin, hipcc tracks the pending LDS write and, unable to
-// tell the ring slots apart, waits vmcnt(0) before every ds_read_b64_tr_b16 it cannot prove
-// disjoint (every MN-contiguous fragment read: the whole K-step pipeline drained each step).
-// The ring's own counted vmcnt waits order these pieces (they count them explicitly); hipcc's
-// waits for its own loads only over-wait when these are hidden from it.  M0 is saved and
-// restored around the piece (hipcc keeps M0 live for its own uses).  No "memory" clobber: a
-// clobber would make hipcc drain vmcnt before it; the volatile asm barriers order it.
-// GVL_DMA_BUILTIN=1 (A/B builds only): the builtin form, i.e. the round-3 code.
-#ifndef GVL_DMA_BUILTIN
-#define GVL_DMA_BUILTIN 0
-#endif
-GVL_DEV void dma16_lds(__amdgpu_buffer_rsrc_t rs, int voff, int soff, const char* lds) {
-#if GVL_DMA_BUILTIN
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, voff, soff, 0, 0);
-  return;
-#endif
-  const uint32_t la = __builtin_amdgcn_readfirstlane(
-      (uint32_t)reinterpret_cast<uintptr_t>((lds_void_t*)lds));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(la), "v"(voff), "s"(rs), "s"(soff));
-}
-
-// The same with 4 B per lane (lds + 4 lane): small per-wave operand fetches beside the ring.
-GVL_DEV void dma4_lds(__amdgpu_buffer_rsrc_t rs, int voff, int soff, const char* lds) {
-  const uint32_t la = __builtin_amdgcn_readfirstlane(
-      (uint32_t)reinterpret_cast<uintptr_t>((lds_void_t*)lds));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-      "buffer_load_dword %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(la), "v"(voff), "s"(rs), "s"(soff));
-}
-
 template <int R, bool MN, int NWV>
 struct Step {
   static constexpr int BYTES = R * KS * 2;
@@ -79,7 +40,8 @@ struct Step {
         const int lc = (lane & 15) ^ fT(kr);
         off_elems = (k0 + kr) * ld + r0 + half * 128 + lc * 8;
       }
-      dma16_lds(rs, (int)(off_elems * 2), 0, lds + j * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + j * 1024), 16,
+                                               (int)(off_elems * 2), 0, 0, 0);
     }
   }
 
@@ -109,7 +71,8 @@ struct Step {
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const int j = t * NWV + wave;
-      dma16_lds(rs, off[t], kbytes, lds + j * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + j * 1024), 16, off[t],
+                                               kbytes, 0, 0);
     }
   }
 
@@ -173,7 +136,9 @@ struct Step192 {
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const int j = t * NWV + wave;
-      if (j < NINSTR) dma16_lds(rs, off[t], kbytes, lds + j * 1024);
+      if (j < NINSTR)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(lds + j * 1024), 16, off[t],
+                                                 kbytes, 0, 0);
     }
   }
   GVL_DEV static short8_t frag(const char* lds, int c0, int lane) {

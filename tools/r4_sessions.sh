@@ -24,27 +24,5 @@ r4a)  # HEAD check + epilogue share of the short-K wide GEMMs (timing-only pp3 b
   diag base 16384 wide all
   for v in pp3d1 pp3d2 base; do diag $v 8064 wide epi; diag $v 16384 wide epi; done
   ;;
-r4b)  # deferred epilogue + asm LDS-DMA: GEMM kernel tests, then A/B shapes and the two steps
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "gemm or batched" --timeout 300 \
-    --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
-  diag dmab 8064 all epi; diag base 8064 all all; GVL_PP3_DEFER=0 diag base 8064 wide epi
-  diag dmab 16384 wide epi; diag base 16384 wide epi
-  for v in dmab base; do
-    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
-    for d in 1 0; do
-      GVL_LIB=$L GVL_PP3_DEFER=$d timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 \
-        --no-cpu-baseline > $O/qf_${v}_d$d.json 2> $O/qf_${v}_d$d.err; fatal $? bench_qf
-      echo "qf $v defer=$d $(python -c "import json;d=json.load(open('$O/qf_${v}_d$d.json'));print(d['value'],d['step_mfma_frac'])")"
-    done
-  done
-  for v in dmab base; do
-    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
-    for d in 1 0; do
-      GVL_LIB=$L GVL_PP3_DEFER=$d timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary \
-        --no-cpu-baseline > $O/lm_${v}_d$d.json 2> $O/lm_${v}_d$d.err; fatal $? bench_lm
-      echo "lm $v defer=$d $(python -c "import json;d=json.load(open('$O/lm_${v}_d$d.json'));print(d['value'],d['step_mfma_frac'])")"
-    done
-  done
-  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
