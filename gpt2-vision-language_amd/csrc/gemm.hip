@@ -208,6 +208,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.drop_thresh = (uint32_t)((double)d->drop_p * 4294967296.0);
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
   p.splits = 1;
+  p.cnt = 0;
   p.bn = 256;
   p.bm = 256;
   p.kper = d->k;

@@ -28,6 +28,7 @@ struct GemmP {
   int bm;     // output tile height of the persistent kernel (256, or 128 with bn 192)
   int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
+  int cnt;  // gemm_pp3_kernel: counted epilogue (set by its launcher, gemm_pp3.h CntEpi)
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
   // writing fp32 partials to ws[s][M][N]; gemm_splitk_reduce applies the epilogue.
   int splits;

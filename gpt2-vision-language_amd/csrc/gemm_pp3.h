@@ -28,6 +28,117 @@ using namespace gvl_ring;
 #ifndef GVL_PP3_DIAG
 #define GVL_PP3_DIAG 0
 #endif
+// s_waitcnt vmcnt(n * PER + X) for a runtime n in [0, MAXN]
+template <int PER, int MAXN, int X>
+GVL_DEV void wait_vm_steps_x(int n) {
+  if (MAXN >= 4 && n >= 4) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PER + X) : "memory"); return; }
+  if (MAXN >= 3 && n == 3) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER + X) : "memory"); return; }
+  if (MAXN >= 2 && n == 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER + X) : "memory"); return; }
+  if (MAXN >= 1 && n == 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER + X) : "memory"); return; }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
+}
+
+// Counted epilogue (kinds without an [M, N] epilogue operand: plain, bias, bias + GELU).  The
+// epilogue's 16-B stores sit in the wave's VMEM queue between the DMA of K-steps c+2 and c+3,
+// so the counted wait at the end of the next NS - 2 phases — "all but the newest two K-steps'
+// pieces" — used to wait for every one of them (a store acknowledgement per tile boundary on
+// the critical path), and the bias, loaded at the tile's first step by a plain load, made
+// hipcc drain the whole DMA queue (vmcnt(0)) at its first use in the epilogue.  Here the
+// stores are buffer stores whose out-of-range lanes get an offset past the buffer (dropped by
+// the range check, no branch), so every epilogue issues exactly CNT_S stores per wave and the
+// NS - 2 following waits count them; the bias row is copied to LDS at kernel start and read by
+// inline asm (with its own lgkmcnt wait) in the epilogue.
+constexpr uint32_t CNT_OOB = 0x7FFFFFF0u;  // voffset past any buffer: the store is dropped
+template <int EPI>
+struct CntEpi {
+  using KD = EpiKind<EPI>;
+  static constexpr bool ON = EPI != EPI_GEN && !KD::AUX && !KD::DROP;
+};
+template <int FM, int FN, int EPI>
+constexpr int cnt_stores() {
+  return FM * (FN / 2 + FN % 2) * (EpiKind<EPI>::ACT ? 2 : 1);
+}
+typedef uint32_t cnt_u32x2 __attribute__((ext_vector_type(2)));
+// the store offset, or the dropped-store offset for an out-of-range lane, made opaque: hipcc
+// would otherwise split the store into two exec-masked branches (one per outcome), which
+// issues a data-dependent number of store instructions
+GVL_DEV uint32_t cnt_off(bool ok, int64_t byte_off) {
+  uint32_t o = ok ? (uint32_t)byte_off : CNT_OOB;
+  asm volatile("" : "+v"(o));
+  return o;
+}
+typedef uint32_t cnt_u32x4 __attribute__((ext_vector_type(4)));
+
+// this wave's bias quads (4 bf16 at columns nw0 + 16 j + 4 (lane >> 4)) from the LDS copy at
+// byte address a (+ 32 j); one asm statement with its lgkmcnt wait (no "memory" clobber: that
+// would make hipcc drain vmcnt in front of it)
+template <int FN>
+GVL_DEV void cnt_bias(uint32_t a, uint2 (&bv)[FN]);
+template <>
+GVL_DEV void cnt_bias<3>(uint32_t a, uint2 (&bv)[3]) {
+  asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:32\n\tds_read_b64 %2, %3 offset:64\n\t"
+               "s_waitcnt lgkmcnt(0)"
+               : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2])
+               : "v"(a));
+}
+template <>
+GVL_DEV void cnt_bias<4>(uint32_t a, uint2 (&bv)[4]) {
+  asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:32\n\tds_read_b64 %2, %4 offset:64\n\t"
+               "ds_read_b64 %3, %4 offset:96\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+               : "v"(a));
+}
+
+// The counted epilogue: gemm_epilogue16's math and lane pairing, buffer stores.
+template <int FM, int FN, int EPI>
+GVL_DEV void gemm_epilogue_cnt(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
+                               int64_t nw0, int lane, float alpha, uint32_t bias_lds,
+                               __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rp) {
+  using KD = EpiKind<EPI>;
+  const int q = lane >> 4;
+  uint2 bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bv[j] = make_uint2(0, 0);
+  if constexpr (KD::BIAS) cnt_bias<FN>(bias_lds + (uint32_t)(2 * (nw0 + 4 * q)), bv);
+  const uint2 z = make_uint2(0, 0);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t m = mw0 + i * 16 + (lane & 15);
+    const bool mok = m < p.M;
+#pragma unroll
+    for (int j = 0; j + 1 < FN; j += 2) {
+      const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
+      float v0[4], v1[4], h0[4] = {0.f, 0.f, 0.f, 0.f}, h1[4] = {0.f, 0.f, 0.f, 0.f};
+      gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, 1.f, bv[j], z, v0, h0);
+      gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, 1.f, bv[j + 1], z, v1, h1);
+      const auto sx = __builtin_amdgcn_permlane16_swap(pack2(v0[0], v0[1]), pack2(v1[0], v1[1]), false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(pack2(v0[2], v0[3]), pack2(v1[2], v1[3]), false, false);
+      const int64_t n = nw0 + 16 * (j + (q & 1)) + 8 * (q >> 1);
+      const bool ok = mok && n < p.N;
+      __builtin_amdgcn_raw_buffer_store_b128(cnt_u32x4{sx[0], sy[0], sx[1], sy[1]}, rc,
+                                             cnt_off(ok, (m * p.ldc + n) * 2), 0, 0);
+      if constexpr (KD::ACT) {
+        const auto hx = __builtin_amdgcn_permlane16_swap(pack2(h0[0], h0[1]), pack2(h1[0], h1[1]), false, false);
+        const auto hy = __builtin_amdgcn_permlane16_swap(pack2(h0[2], h0[3]), pack2(h1[2], h1[3]), false, false);
+        __builtin_amdgcn_raw_buffer_store_b128(cnt_u32x4{hx[0], hy[0], hx[1], hy[1]}, rp,
+                                               cnt_off(ok, (m * p.ldp + n) * 2), 0, 0);
+      }
+    }
+    if constexpr (FN % 2 == 1) {
+      constexpr int j = FN - 1;
+      const int64_t n0 = nw0 + j * 16 + 4 * q;
+      float v0[4], h0[4] = {0.f, 0.f, 0.f, 0.f};
+      gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, 1.f, bv[j], z, v0, h0);
+      const bool ok = mok && n0 < p.N;
+      __builtin_amdgcn_raw_buffer_store_b64(cnt_u32x2{pack2(v0[0], v0[1]), pack2(v0[2], v0[3])}, rc,
+                                            cnt_off(ok, (m * p.ldc + n0) * 2), 0, 0);
+      if constexpr (KD::ACT)
+        __builtin_amdgcn_raw_buffer_store_b64(cnt_u32x2{pack2(h0[0], h0[1]), pack2(h0[2], h0[3])}, rp,
+                                              cnt_off(ok, (m * p.ldp + n0) * 2), 0, 0);
+    }
+  }
+}
+
 template <int BN, bool BMN>
 struct SlabB {
   using type = Step<256, BMN, 8>;
@@ -142,6 +253,26 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
   bool do_db = false;
+  // counted epilogue (CntEpi): single-problem launches; the bias row in LDS after the ring
+  constexpr bool CNT = CntEpi<EPI>::ON;
+  constexpr int CNT_S = cnt_stores<FM, FN, EPI>();
+  static_assert(!CNT || (NS - 2) * (IPW0 > IPW1 ? IPW0 : IPW1) + CNT_S <= 63, "vmcnt range");
+  const bool cnt_on = CNT && p.cnt && GVL_PP3_DIAG == 0;
+  const uint32_t bias_lds = (uint32_t)(NS * SLOT);
+  const __amdgpu_buffer_rsrc_t rc_cnt = uniform_rsrc(p.C, CNT ? p.M * p.ldc * 2 : 0);
+  const __amdgpu_buffer_rsrc_t rp_cnt =
+      uniform_rsrc(EpiKind<EPI>::ACT ? p.pre_out : p.C, CNT && EpiKind<EPI>::ACT ? p.M * p.ldp * 2 : 0);
+  if constexpr (CNT && EpiKind<EPI>::BIAS) {  // plain loads here, before any LDS-DMA is in flight
+    if (cnt_on)
+      for (int n = tid * 8; n < p.N; n += 512 * 8)
+        *reinterpret_cast<uint4*>(smem + NS * SLOT + 2 * n) = *reinterpret_cast<const uint4*>(p.bias + n);
+  }
+  int cnt_w = 0;  // waits left that must count the last counted epilogue's stores
+  // alpha (x *alpha_ptr, a device scalar written before this launch) read once up front: a
+  // load inside the loop would make hipcc drain the DMA queue (vmcnt(0)) at every epilogue,
+  // and here, before the first DMA, its wait drains nothing
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i) GVL_PP3_ISSUE(i);
   {
@@ -152,16 +283,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
   barrier_lds();
   if (g == 1) __builtin_amdgcn_s_barrier();
 
-  // alpha (x *alpha_ptr, a device scalar written before this launch) read once up front: a
-  // load inside the loop would make hipcc drain the DMA queue (vmcnt(0)) at every epilogue
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   int cu_t = 0, cu_k = 0;  // compute cursor
   int64_t cu_m0, cu_n0, cu_k0;
   int cu_sp, cu_bi;
   tile_coords(0, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
   EpiPre<FM, FN, EPI> pre;
-  pre.load_bias(p, cu_n0 + bcol, lane);
+  if (!cnt_on) pre.load_bias(p, cu_n0 + bcol, lane);
   if constexpr (DB) do_db = p.batch > 1 && p.splits == 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
 #define GVL_PP3_EPILOGUE()                                                                   \
   do {                                                                                       \
@@ -188,6 +315,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
         _Pragma("unroll") for (int i_ = 0; i_ < FM; ++i_)                                    \
           _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                                  \
             asm volatile("" ::"v"(acc[i_][j_]));                                             \
+      } else if (CNT && cnt_on) {                                                            \
+        gemm_epilogue_cnt<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha,       \
+                                       bias_lds, rc_cnt, rp_cnt);                            \
+        cnt_w = NS - 2;                                                                      \
       } else {                                                                               \
         gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_, \
                                      p.batch > 1 ? static_cast<const bf16_t*>(c_) : p.residual); \
@@ -216,7 +347,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
         for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
       ++cu_t;
       tile_coords(cu_t, cu_m0, cu_n0, cu_k0, cu_sp, cu_bi);
-      pre.load_bias(p, cu_n0 + bcol, lane);
+      if (!cnt_on) pre.load_bias(p, cu_n0 + bcol, lane);
       if constexpr (DB) do_db = p.batch > 1 && p.splits == 1 && cu_n0 == 0 && p.Db[cu_bi] != nullptr;
     }
     const char* sl = smem + (c % NS) * SLOT;
@@ -227,7 +358,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     GVL_PP3_ISSUE(c + NS - 1);
     {
       const int r = nsteps - (c + 2);  // steps issued but not needed by step c+1
-      if (g == 1) wait_vm_steps<IPW1, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+      const int n_ = r < 0 ? 0 : (r < NS - 2 ? r : NS - 2);
+      if (g == 1) {
+        if (CNT && cnt_w > 0) {  // the last epilogue's CNT_S stores are younger than step c+1
+          wait_vm_steps_x<IPW1, NS - 2, CNT_S>(n_);
+          --cnt_w;
+        } else {
+          wait_vm_steps<IPW1, NS - 2>(n_);
+        }
+      }
     }
     barrier_lds();
     // ---- C(c)
@@ -251,7 +390,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
     if (++cu_k == nks) cu_k = 0;
     {
       const int r = nsteps - (c + 2);
-      if (g == 0) wait_vm_steps<IPW0, NS - 2>(r < 0 ? 0 : (r < NS - 2 ? r : NS - 2));
+      const int n_ = r < 0 ? 0 : (r < NS - 2 ? r : NS - 2);
+      if (g == 0) {
+        if (CNT && cnt_w > 0) {
+          wait_vm_steps_x<IPW0, NS - 2, CNT_S>(n_);
+          --cnt_w;
+        } else {
+          wait_vm_steps<IPW0, NS - 2>(n_);
+        }
+      }
     }
     barrier_lds();
   }
@@ -264,11 +411,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
 template <int NS, bool AMN, bool BMN, int EPI, int BN, int BM>
 int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
   GemmP p = p0;  // tiles_m/n, splits, kper set by gemm_pp3_try
-  constexpr int lds = NS * (BM + BN) * KS * 2;
+  // counted epilogue (CntEpi): one problem, 32-bit store offsets below the dropped-store offset,
+  // a 16-B aligned bias row whose LDS copy fits after the ring (GVL_PP3_CNT=0: off, A/B)
+  static const bool cnt_env = [] {
+    const char* e = getenv("GVL_PP3_CNT");
+    return !(e && e[0] == '0');
+  }();
+  constexpr int ring = NS * (BM + BN) * KS * 2;
+  const int64_t bias_bytes = EpiKind<EPI>::BIAS ? 2 * (int64_t)p.tiles_n * BN : 0;
+  p.cnt = CntEpi<EPI>::ON && cnt_env && p.batch == 1 && ring + bias_bytes <= 160 * 1024 &&
+          p.M * p.ldc * 2 <= (int64_t)CNT_OOB &&
+          (!EpiKind<EPI>::ACT || (p.pre_out != nullptr && p.M * p.ldp * 2 <= (int64_t)CNT_OOB)) &&
+          (!EpiKind<EPI>::BIAS || ((reinterpret_cast<uintptr_t>(p.bias) & 15) == 0 && p.N % 8 == 0));
+  const int lds = ring + (p.cnt ? (int)bias_bytes : 0);
   auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI, BN, BM>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int total = p.tiles_m * p.tiles_n * p.splits * p.batch;

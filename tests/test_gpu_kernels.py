@@ -158,6 +158,52 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])
+@pytest.mark.parametrize("M,N,K", [(8064, 3072, 768), (7999, 2240, 768), (16384, 768, 3072),
+                                   (4096, 2304, 768), (2048, 50304, 768)])
+def test_gemm_counted_epilogue(cuda, epi, M, N, K):
+    """Counted epilogue of the persistent kernel (gemm_pp3.h CntEpi: bias row in LDS, buffer
+    stores with dropped out-of-range lanes, the next NS - 2 waits counting them): every kind
+    it takes, ragged M and N (M-tail rows, a partial last column tile), several tiles per CU,
+    the lm_head width; vs the fp32 product + bias (+ GELU / gelu'), and a sentinel-bordered
+    output for the tails."""
+    K_ = _k()
+    if epi == "bias" and N > 4096:
+        pytest.skip("lm_head carries no bias")
+    torch.manual_seed(M + N + K + len(epi))
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A, B = a.to(cuda), b.t().contiguous().to(cuda)
+    name = _kernel_name(A, B, 0, 0, M, N, K, epi={"bias_act_erf_d": "bias_act_d"}.get(epi, epi))
+    assert name.startswith("gemm_pp3_kernel"), name
+    bias = torch.randn(N).to(BF)
+    h = a.float() @ b.float() + (0 if epi == "plain" else bias.float())
+    kw, ref = {}, h
+    if epi == "bias":
+        kw = dict(bias=bias.to(cuda))
+    elif epi != "plain":
+        erf = epi == "bias_act_erf_d"
+        x = h.clone().requires_grad_(True)
+        g = O.gelu_erf(x) if erf else O.gelu_tanh(x)
+        g.sum().backward()
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        kw, ref = dict(bias=bias.to(cuda), act=4 if erf else 3, pre_out=pre), g.detach()
+    y = K_.gemm(A, B, **kw)
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+    if "pre_out" in kw:
+        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
+    if M % 256 or N % 192:  # tail stores must not land outside the output
+        big = torch.full((M + 3, N + 64), 7.0, dtype=BF, device=cuda)
+        if "pre_out" in kw:
+            pbig = torch.full((M + 3, N + 64), 7.0, dtype=BF, device=cuda)
+            kw["pre_out"] = pbig[:M, :N]
+        K_.gemm(A, B, out=big[:M, :N], **kw)
+        assert torch.all(big[M:] == 7.0) and torch.all(big[:, N:] == 7.0)
+        assert torch.equal(big[:M, :N], y)
+        if "pre_out" in kw:
+            assert torch.all(pbig[M:] == 7.0) and torch.all(pbig[:, N:] == 7.0)
+
+
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("epi", ["plain", "bias_res", "res_inplace", "bias_act", "dact"])
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (12000, 1536, 320), (16384, 2304, 32)])

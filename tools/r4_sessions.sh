@@ -24,5 +24,17 @@ r4a)  # HEAD check + epilogue share of the short-K wide GEMMs (timing-only pp3 b
   diag base 16384 wide all
   for v in pp3d1 pp3d2 base; do diag $v 8064 wide epi; diag $v 16384 wide epi; done
   ;;
+r4c)  # counted epilogue: GEMM kernel tests, then A/B (GVL_PP3_CNT=1 default / 0) on shapes and steps
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "gemm or batched" --timeout 300 \
+    --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  for c in 1 0; do GVL_PP3_CNT=$c diag base 8064 all epi; mv $O/diag_base_8064_all.log $O/diag_c${c}_8064.log
+    GVL_PP3_CNT=$c diag base 16384 wide epi; mv $O/diag_base_16384_wide.log $O/diag_c${c}_16384.log; done
+  for w in qformer lm; do for c in 1 0; do
+    a="--workload qformer --steps 10 --warmup 3"; [ $w = lm ] && a="--steps 2 --warmup 1 --no-secondary"
+    GVL_PP3_CNT=$c timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/${w}_c$c.json 2> $O/${w}_c$c.err
+    fatal $? bench_$w
+    echo "$w cnt=$c $(python -c "import json;d=json.load(open('$O/${w}_c$c.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
