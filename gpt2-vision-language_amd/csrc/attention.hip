@@ -343,26 +343,6 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
   (void)l;
 }
 
-// ------------------------------------------------------------------------------------
-// D[b,h,q] = sum_d dO*O  (one thread per row, 8 x 16-B loads each)
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnP p, AttnG g) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = p.B * p.H * p.Tq;
-  if (idx >= total) return;
-  const int64_t q = idx % p.Tq, bh = idx / p.Tq, h = bh % p.H, b = bh / p.H;
-  const bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q * p.o_st;
-  const bf16_t* drow = g.dout + b * g.do_sb + h * g.do_sh + q * g.do_st;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const uint4 a = *reinterpret_cast<const uint4*>(orow + c * 8);
-    const uint4 d = *reinterpret_cast<const uint4*>(drow + c * 8);
-    s += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
-         hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
-         lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
-  }
-  g.Dws[idx] = s;
-}
 
 // dK/dV, LDS-DMA pipelined (Tk > 64): block = (64-key tile, head, batch); the Q / dO tiles
 // and their lse / D rows move global -> LDS by buffer_load ... lds (no staging registers)
@@ -385,14 +365,21 @@ GVL_DEV short8_t frag_tr_asm(const char* lds, int t, int s, int lane) {
   const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
   const uint32_t oa = base + swz_tr(ra, ch) + (p & 1) * 8, ob = base + swz_tr(rb, ch) + (p & 1) * 8;
   short4_t lo, hi;
+  // early-clobber outputs: without "&" the register allocator may put lo over ob (it did, in
+  // the dQ and dK/dV kernels), and the second read then takes its address from a register the
+  // first read is filling; when that read returns before the second issues (LDS queue backed
+  // up), the second read fetches from a wrong LDS address — round 3's intermittent wrong dQ
   asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
-               : "=v"(lo), "=v"(hi) : "v"(oa), "v"(ob) : "memory");
+               : "=&v"(lo), "=&v"(hi) : "v"(oa), "v"(ob) : "memory");
   short8_t r;
   r.lo = lo;
   r.hi = hi;
   return r;
 }
 // lgkmcnt(0), with the fragments threaded through so no use is scheduled above the wait
+GVL_DEV void lds_wait4(short8_t (&a)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : : "memory");
+}
 GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
@@ -526,7 +513,7 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
         // (the whole two-ahead prefetch) before a plain read; they landed before the barrier.
         float4_t l4, d4;
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(l4), "=v"(d4)
+                     : "=&v"(l4), "=&v"(d4)  // early-clobber: l4 must not sit on the address
                      : "v"((uint32_t)reinterpret_cast<uintptr_t>(sl + 16 * n + 4 * Gl))
                      : "memory");
 #pragma unroll
@@ -592,9 +579,11 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
 // dQ, LDS-DMA pipelined (Tq > 64): block = (64*G-query tile, head, batch), each wave G groups
 // of 16 query rows; the K / V tiles move global -> LDS by buffer_load ... lds into a 3-slot ring two key tiles ahead (as
 // attn_bwd_dkdv_dma_kernel; transposed K reads by inline asm for the same reason).
-// D = rowsum(dO * O) comes from attn_bwd_pre_kernel.  (Computing it inside this kernel from
-// the dO fragments it holds gave intermittently wrong dQ — 4 of 40 repeats of a dropout case
-// with NaN-filled free memory, tools/r3/attn_stress.py — and was reverted.)
+// It also computes D = rowsum(dO * O) (no separate pre-pass launch): each lane holds 16 of
+// its row's 64 dO values as MFMA fragments, loads the matching O values, and the row's four
+// lanes reduce by two shuffles; D goes to the workspace for the dK/dV kernel that runs next.
+// (Round 3's first version of this gave intermittently wrong dQ; the cause was frag_tr_asm's
+// missing early-clobber — see there — which the fused variant's timing exposed.)
 template <int G, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG gg) {
   using gvl_ring::lds_void_t;
@@ -627,8 +616,26 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     }
     const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
     lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
-    Dq[g] = qok[g] ? gg.Dws[ridx] : 0.f;
     drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
+  }
+  {  // D = rowsum(dO * O): this lane's 16 dims (8 at 32 s2 + 8 Gl, s2 = 0, 1), then the row's 4 lanes
+    const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float sd = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t of = load_frag_global(obase + q[g] * p.o_st, s2, lane, qok[g]);
+        const uint4 ou = __builtin_bit_cast(uint4, of), du = __builtin_bit_cast(uint4, df[g][s2]);
+        const uint32_t ow[4] = {ou.x, ou.y, ou.z, ou.w}, dw[4] = {du.x, du.y, du.z, du.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sd += lo_bf(ow[k]) * lo_bf(dw[k]) + hi_bf(ow[k]) * hi_bf(dw[k]);
+      }
+      sd += __shfl_xor(sd, 16, 64);
+      sd += __shfl_xor(sd, 32, 64);
+      Dq[g] = qok[g] ? sd : 0.f;
+      if (qok[g] && Gl == 0) gg.Dws[(b * p.H + h) * p.Tq + q[g]] = sd;
+    }
   }
   int64_t kend = p.Tk;
   if (p.causal) {
@@ -712,12 +719,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      short8_t kt4[4], kt4b[4];
+      short8_t kt4[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) kt4[t] = frag_tr_asm(ks, t, s2, lane);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) kt4b[t] = kt4[t];
-      lds_wait8(kt4, kt4b);
+      lds_wait4(kt4);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1003,10 +1008,7 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
     GVL_LAUNCH_CHECK("gvl_attn_bwd(short)");
     return 0;
   }
-  // D = rowsum(dO * O) into the workspace, dQ, then dK/dV
-  const int64_t rows = d->B * d->H * d->Tq;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p, g);
-  GVL_LAUNCH_CHECK("gvl_attn_bwd(pre)");
+  // dQ (which also writes D = rowsum(dO * O) into the workspace), then dK/dV
   const int Gq = pick_groups(d->Tq);
   dim3 gq(grid_1d(d, (d->Tq + 64 * Gq - 1) / (64 * Gq)));
   if (Gq == 2) {

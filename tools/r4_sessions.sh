@@ -36,5 +36,22 @@ r4c)  # counted epilogue: GEMM kernel tests, then A/B (GVL_PP3_CNT=1 default / 0
     echo "$w cnt=$c $(python -c "import json;d=json.load(open('$O/${w}_c$c.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done; done
   ;;
+r4d)  # early-clobber fix + fused D re-landed: GPU suite once, smoke, the driver's default bench
+  suite
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],[(k,v.get('value')) for k,v in d.get('secondary',{}).items()] if isinstance(d.get('secondary'),dict) else '')"
+  ;;
+r4e)  # rocprof kernel stats of both steps at this head; Q-Former DP overlap traces (world-1 RCCL)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  for w in qf lm; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -25 $O/${w}_table.txt; done
+  for mb in 32 8; do for mode in qf_eager qf_graph; do
+    GVL_BUCKET_MB=$mb GVL_TRACE_BUCKETS=1 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --output-format csv \
+      -d $O/dp_${mode}_$mb -o dp -- python tools/dp_overlap_trace.py $mode > $O/dp_${mode}_$mb.log 2>&1; fatal $? dp_$mode
+    python tools/dp_overlap_report.py $O/dp_${mode}_$mb > $O/dp_overlap_${mode}_$mb.txt 2>&1; echo "== $mode $mb MB"; head -12 $O/dp_overlap_${mode}_$mb.txt
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
