@@ -421,6 +421,9 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
       vf[g][s2] = load_frag_global(vbase + key[g] * p.v_st, s2, lane, kok[g]);
     }
   }
+  // K / V fragments landed before the ring's first DMA (else hipcc drains the ring at the loop entry)
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" ::"v"(kf[g][0]), "v"(kf[g][1]), "v"(vf[g][0]), "v"(vf[g][1]));
   const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
   const int nqt = (int)((p.Tq + KT - 1) / KT);
   const int nq = nqt - qt_first;
@@ -748,6 +751,177 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
   }
 }
 
+// Forward, LDS-DMA pipelined (no dropout, more than one key tile: the LM's T = 1024): the
+// query tile stays in registers while the K / V tiles stream global -> LDS by buffer_load ...
+// lds into a 3-slot ring two key tiles ahead (attn_bwd_dq_dma_kernel's ring: same 1-KiB
+// pieces, source-side swizzle, counted vmcnt), instead of attn_fwd_kernel's register staging
+// one tile ahead (its timing-only build without the staging ran 18 % faster).  V is read
+// transposed by frag_tr_asm (a builtin transposed read would make hipcc drain the DMA queue).
+// Math as attn_fwd_kernel<G, false> (deferred rescale, the row sum from a ones MFMA).
+template <int G>
+__global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
+  using gvl_ring::lds_void_t;
+  constexpr int QT = 64 * G, SLOT = 2 * KT * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];  // [slot][K, V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Gl = lane >> 4;
+  int64_t qt, h, b;
+  tile_of_block<true>(p, (p.Tq + QT - 1) / QT, qt, h, b);
+  const int64_t qblk0 = qt * QT;
+  const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
+  const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
+  int64_t q[G];
+  bool qok[G];
+  short8_t qf[G][2];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
+    qok[g] = q[g] < p.Tq;
+    qf[g][0] = load_frag_global(qbase + q[g] * p.q_st, 0, lane, qok[g]);
+    qf[g][1] = load_frag_global(qbase + q[g] * p.q_st, 1, lane, qok[g]);
+  }
+  // the Q fragments land before the first DMA is issued: waited for at their first use, they
+  // would make hipcc drain the whole prefetched ring (vmcnt(0)) at the loop entry
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" ::"v"(qf[g][0]), "v"(qf[g][1]));
+  int64_t kend = p.Tk;
+  if (p.causal) {
+    const int64_t lim = qblk0 + QT;
+    if (lim < kend) kend = lim;
+  }
+  const int nkt = (int)((kend + KT - 1) / KT);
+  constexpr int NO = 5;  // o[g][4]: row sum of the bf16 P (ones MFMA)
+  float4_t o[G][NO];
+  float m[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int t = 0; t < NO; ++t) o[g][t] = float4_t{0.f, 0.f, 0.f, 0.f};
+    m[g] = -INFINITY;
+  }
+  short8_t ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
+  const __amdgpu_buffer_rsrc_t rk = gvl_ring::uniform_rsrc(kbase, ((p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = gvl_ring::uniform_rsrc(vbase, ((p.Tk - 1) * p.v_st + D) * 2);
+  auto issue = [&](int kt, int slot) {  // 4 DMA instructions per wave
+    char* sb = smem + slot * SLOT;
+    const int64_t k0 = (int64_t)kt * KT;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = 2 * wave + t;
+      const int row = 8 * j + (lane >> 3);
+      const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+      const int vok = (int)(((k0 + row) * p.k_st + chunk * 8) * 2);
+      const int vov = (int)(((k0 + row) * p.v_st + chunk * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void_t*)(sb + j * 1024), 16, vok, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void_t*)(sb + KT * D * 2 + j * 1024), 16,
+                                               vov, 0, 0, 0);
+    }
+  };
+  if (nkt > 0) {
+    issue(0, 0);
+    if (nkt > 1) issue(1, 1);
+    if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    gvl_ring::barrier_lds();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
+    const char* ks = smem + (kt % 3) * SLOT;
+    const char* vs = ks + KT * D * 2;
+    const int64_t k0 = (int64_t)kt * KT;
+    float4_t sc[G][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t kf = frag_row(ks, 16 * n, s2, lane);
+#pragma unroll
+        for (int g = 0; g < G; ++g) sc[g][n] = mfma16(kf, qf[g][s2], sc[g][n]);
+      }
+    }
+    short8_t pf[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
+      if (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0)) {
+        const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kk = 16 * n + 4 * Gl + r;
+            if (kk >= kl || (p.causal && kk > ql)) sc[g][n][r] = -INFINITY;
+          }
+      }
+      float mx = fmaxf(fmaxf(sc[g][0][0], sc[g][0][1]), sc[g][0][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][0][3]), sc[g][1][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][1][1]), sc[g][1][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][1][3]), sc[g][2][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][2][1]), sc[g][2][2]);
+      mx = fmaxf(fmaxf(mx, sc[g][2][3]), sc[g][3][0]);
+      mx = fmaxf(fmaxf(mx, sc[g][3][1]), sc[g][3][2]);
+      mx = fmaxf(mx, sc[g][3][3]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      constexpr float RESCALE_LOG2 = 4.f;  // deferred rescale, as attn_fwd_kernel
+      const float cand = mx * p.c2;
+      if (!__all(cand - m[g] <= RESCALE_LOG2)) {
+        const float mnew = fmaxf(m[g], cand);
+        const float msub0 = (mnew == -INFINITY) ? 0.f : mnew;
+        const float alpha = __builtin_amdgcn_exp2f(m[g] - msub0);
+        m[g] = mnew;
+#pragma unroll
+        for (int t = 0; t < NO; ++t) o[g][t] *= alpha;
+      }
+      const float msub = (m[g] == -INFINITY) ? 0.f : m[g];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[g][n][r] = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -msub));
+      pf[g][0] = pack_frag(sc[g][0], sc[g][1]);
+      pf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      short8_t vf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vf[t] = frag_tr_asm(vs, t, s2, lane);
+      lds_wait4(vf);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) o[g][t] = mfma16(vf[t], pf[g][s2], o[g][t]);
+#pragma unroll
+      for (int g = 0; g < G; ++g) o[g][4] = mfma16(ones, pf[g][s2], o[g][4]);
+    }
+    if (kt + 1 < nkt) {
+      if (kt + 2 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gvl_ring::barrier_lds();
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float lt = o[g][4][0];
+    if (!qok[g]) continue;
+    const float inv = 1.f / lt;
+    bf16_t* orow = p.o + b * p.o_sb + h * p.o_sh + q[g] * p.o_st;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int d = 16 * t + 4 * Gl;
+      *reinterpret_cast<uint2*>(orow + d) = make_uint2(pack2(o[g][t][0] * inv, o[g][t][1] * inv),
+                                                       pack2(o[g][t][2] * inv, o[g][t][3] * inv));
+    }
+    if (Gl == 0 && p.lse) p.lse[(b * p.H + h) * p.Tq + q[g]] = (m[g] + log2f(lt)) * LN2;
+  }
+}
+
 // Short sequences (Tq, Tk <= 64: the caption decoder's 63 tokens, the Q-Former's 32 queries
 // over 32 / 33 tokens): the whole backward of one (b, h) in one block, no recompute.
 // Q, K, V, dO land in LDS once; phase 1 (wave w = queries 16w..16w+15) computes D = rowsum(dO O),
@@ -955,6 +1129,16 @@ bool short_bwd_enabled() {
   return on;
 }
 
+// LDS-DMA forward (attn_fwd_dma_kernel) for multi-tile key ranges without dropout;
+// GVL_ATTN_FWD_DMA=0: the register-staged attn_fwd_kernel (A/B).
+bool fwd_dma_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_ATTN_FWD_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Block count of the 1-D heavy-first grid (see tile_of_block); fill() bounds it.
 unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntile * d->H * d->B); }
 
@@ -966,7 +1150,10 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   const int G = pick_groups(d->Tq);
   dim3 grid(grid_1d(d, (d->Tq + 64 * G - 1) / (64 * G)));
   hipStream_t s = gvl::as_stream(stream);
-  if (G == 2) {
+  if (!p.has_drop && d->Tk > KT && fwd_dma_enabled()) {
+    if (G == 2) gvl::launch_timed(attn_fwd_dma_kernel<2>, grid, dim3(NT), 0, s, p);
+    else gvl::launch_timed(attn_fwd_dma_kernel<1>, grid, dim3(NT), 0, s, p);
+  } else if (G == 2) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
   } else {

@@ -733,7 +733,7 @@ def test_attention_causal(cuda, B, H, T):
     _attn_case(cuda, B, H, T, T, True, packed=True)
 
 
-@pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257)])
+@pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257), (40, 130), (130, 1000)])
 def test_attention_noncausal(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False)
 

@@ -53,5 +53,12 @@ r4e)  # rocprof kernel stats of both steps at this head; Q-Former DP overlap tra
     python tools/dp_overlap_report.py $O/dp_${mode}_$mb > $O/dp_overlap_${mode}_$mb.txt 2>&1; echo "== $mode $mb MB"; head -12 $O/dp_overlap_${mode}_$mb.txt
   done; done
   ;;
+r4f)  # batched weight gradients vs the hipBLASLt yardstick; N = 768 shapes on the persistent kernel
+  timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad.log 2>&1; rc=$?; cat $O/wgrad.log; fatal $rc wgrad
+  diag base 8064 narrow all; mv $O/diag_base_8064_narrow.log $O/diag_def_8064n.log
+  GVL_GEMM_CFG=3 diag base 8064 narrow all; mv $O/diag_base_8064_narrow.log $O/diag_pp3_8064n.log
+  GVL_GEMM_CFG=3 diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_pp3_16384n.log
+  diag base 16384 narrow all
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

@@ -1,0 +1,58 @@
+"""Batched weight-gradient GEMMs of the LM step (gvl_gemm_batched, one persistent launch for
+the 12 blocks' dW += dY^T X of one shape, fused bias column sums) against the hipBLASLt
+yardstick (torch.bmm over the same transposed views, no accumulate, no bias), HIP events,
+median of 5 x 10 launches.  python tools/wgrad_diag.py [K]  (K = tokens per micro-step,
+default 16384 = B 16 x T 1024)."""
+import os
+import ctypes as C
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gpt2-vision-language_amd")]
+from gvl import _lib  # noqa: E402
+from gvl import kernels as K  # noqa: E402
+
+_lib.load()
+dev = torch.device("cuda:0")
+KT = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+L = 12
+SHAPES = [("c_attn", 2304, 768), ("attn.c_proj", 768, 768), ("c_fc", 3072, 768), ("mlp.c_proj", 768, 3072)]
+
+
+def timeit(fn, reps=10, rounds=5):
+    t = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1) * 1e3 / reps)
+    return statistics.median(t)
+
+
+torch.manual_seed(0)
+for name, M, N in SHAPES:
+    dy = [(torch.rand(KT, M, device=dev) - 0.5).to(torch.bfloat16) for _ in range(L)]
+    x = [(torch.rand(KT, N, device=dev) - 0.5).to(torch.bfloat16) for _ in range(L)]
+    g = [torch.zeros(M, N, device=dev, dtype=torch.bfloat16) for _ in range(L)]
+    db = [torch.zeros(M, device=dev, dtype=torch.bfloat16) for _ in range(L)]
+    items = [(dy[i], x[i], g[i], True) for i in range(L)]
+    fl = 2.0 * M * N * KT * L
+    tb = timeit(lambda: K.gemm_batched(items, a_mn=True, b_mn=True, dbias=db))
+    tn = timeit(lambda: K.gemm_batched(items, a_mn=True, b_mn=True))
+    K.gemm_batched(items, a_mn=True, b_mn=True)
+    buf = C.create_string_buffer(128)
+    _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
+    kname = buf.value.decode()
+    DY, X = torch.stack(dy), torch.stack(x)
+    ty = timeit(lambda: torch.bmm(DY.transpose(1, 2), X))
+    print(f"{name:12s} M={M:5d} N={N:5d} K={KT} x{L}: gvl+dbias {tb:8.1f}us ({fl / tb / 1e6:6.0f} TF/s)  "
+          f"gvl {tn:8.1f}us ({fl / tn / 1e6:6.0f} TF/s)  torch.bmm {ty:8.1f}us ({fl / ty / 1e6:6.0f} TF/s)  [{kname}]",
+          flush=True)
+    del dy, x, g, db, items, DY, X
+    torch.cuda.empty_cache()
