@@ -60,5 +60,15 @@ r4f)  # batched weight gradients vs the hipBLASLt yardstick; N = 768 shapes on t
   GVL_GEMM_CFG=3 diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_pp3_16384n.log
   diag base 16384 narrow all
   ;;
+r4g)  # attention forward: LDS-DMA ring vs register staging (GVL_ATTN_FWD_DMA), alternated
+  for r in 1 2; do for f in 1 0; do
+    GVL_ATTN_FWD_DMA=$f timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_f${f}_$r.log 2>&1; fatal $? attn
+    echo "fwd_dma=$f round $r"; head -3 $O/attn_f${f}_$r.log
+  done; done
+  for f in 1 0; do
+    GVL_ATTN_FWD_DMA=$f timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_f$f.json 2> $O/lm_f$f.err
+    fatal $? bench_lm; echo "lm fwd_dma=$f $(python -c "import json;d=json.load(open('$O/lm_f$f.json'));print(d['value'])")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
