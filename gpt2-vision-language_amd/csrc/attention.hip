@@ -9,9 +9,10 @@
 // The output accumulator keeps the same query on the lane, so rescales are lane-local.
 // With G = 2 every K/V fragment read from LDS feeds two MFMAs (two query groups).
 //
-// Backward (FA2 recompute, no atomics, deterministic): D = rowsum(dO*O) by a row pass; dQ by a
-// query-tile kernel looping over key tiles; dK/dV by a key-tile kernel (16 keys per wave)
-// looping over query tiles; both stage their streamed tiles by LDS-DMA.  Sequences of <= 64 rows take one fused kernel.  P is recomputed from the saved
+// Backward (FA2 recompute, no atomics, deterministic): dQ by a query-tile kernel looping over
+// key tiles, which also writes D = rowsum(dO*O); dK/dV by a key-tile kernel (16 keys per wave)
+// looping over query tiles; both stage their streamed tiles by LDS-DMA (so does the no-dropout
+// forward, attn_fwd_dma_kernel).  Sequences of <= 64 rows take one fused kernel.  P is recomputed from the saved
 // log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash mask on (b,h,q,k), identical in
 // every kernel.
 #include <algorithm>
