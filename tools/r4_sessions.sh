@@ -74,5 +74,14 @@ r4h)  # PMC passes of both bench steps (HBM bytes, MFMA busy, achieved clock per
   bash tools/pmc_traffic.sh $S; rc=$?; fatal $rc pmc
   python -c "import json;d=json.load(open('gpurun_out/pmc_traffic_$S.json'));[print(w,k,v) for w in d['workloads'] for k,v in sorted(d['workloads'][w].items(),key=lambda kv:-kv[1].get('launches',0))[:6]]"
   ;;
+r4i)  # which hipBLASLt kernels (macro tile, MFMA, depth) beat the persistent / direct-A GEMMs on N = 768
+  for M in 16384 8064; do
+    GVL_DIAG_COLS=all timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_diag_$M -o diag -- \
+      python tools/gemm_diag.py $M narrow > $O/diag_$M.log 2>&1; fatal $? prof_diag
+    f=$(find $O/prof_diag_$M -name "*kernel_stats.csv" | head -1)
+    python -c "import csv,sys;rows=sorted(csv.DictReader(open(sys.argv[1])),key=lambda r:-float(r['TotalDurationNs']));[print(r['Calls'],round(float(r['AverageNs'])/1e3,2),r['Name'][:400]) for r in rows[:30]]" $f > $O/diag_table_$M.txt
+    cat $O/diag_table_$M.txt
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
