@@ -233,6 +233,10 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
+  if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_routed(d)) {
+    snprintf(buf, len, "hipblaslt");
+    return 0;
+  }
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     GemmP p;
     fill_params(d, p);
@@ -291,6 +295,10 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GemmP p;
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
+  if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_try(d, s)) {  // plain GEMM on hipBLASLt
+    GVL_LAUNCH_CHECK("gvl_gemm(hipblaslt)");
+    return 0;
+  }
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     const int cfg = env().cfg;
     GemmP q = p;

@@ -500,5 +500,7 @@ int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_rows128(const GemmP& p);  // the launch uses 128-row tiles (gemm_w4m_kernel)
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 bool gemm_w4d_ok(const GemmP& p);  // gemm_w4d.hip: direct-A variant for a w4-planned shape
+bool gemm_lib_routed(const gvl_gemm_desc* d);         // gemm_lib.cpp: plain GEMM for hipBLASLt
+bool gemm_lib_try(const gvl_gemm_desc* d, hipStream_t s);  // launched there (else false)
 int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s);
 }  // namespace gvl

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 7
+#define GVL_ABI_VERSION 8
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -122,6 +122,12 @@ int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len);
  * gvl_gemm_batched_dbias call launched as one batched launch ("" when it ran the problems one
  * by one through gvl_gemm): the bench attributes the batched weight-gradient launches too. */
 int gvl_gemm_batched_kernel_name(char* buf, int32_t len);
+/* ABI v8: plain GEMMs (no bias / activation / residual / dropout / gate / alpha_ptr, bf16 C)
+ * of the shapes where hipBLASLt's kernel is measured faster (N = 768 with 768 <= K <= 4096 and
+ * the lm_head forward, M >= 4096) run on hipBLASLt from inside gvl_gemm (impl 3, cfg -1);
+ * gvl_gemm_kernel_name reports "hipblaslt" for them.  mode 0 = never, 1 = those shapes
+ * (default; env GVL_GEMM_LIB), 2 = every plain GEMM (tests).  Returns the previous mode. */
+int gvl_gemm_lib_route(int32_t mode);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (eps given; reference uses 1e-5).

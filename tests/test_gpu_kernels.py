@@ -22,6 +22,22 @@ def _k():
     return K
 
 
+@pytest.fixture(autouse=True)
+def _own_gemm_kernels(request):
+    """The tests here exercise gvl's own GEMM kernels, so the plain GEMMs that gvl_gemm routes
+    to hipBLASLt by default (gemm_lib.cpp) run on them (gvl_gemm_lib_route(0)), except in
+    test_gemm_library_route*, which covers the routed path."""
+    if request.node.name.startswith("test_gemm_library_route"):
+        yield
+        return
+    from gvl import _lib
+    prev = _lib.lib().gvl_gemm_lib_route(0)
+    try:
+        yield
+    finally:
+        _lib.lib().gvl_gemm_lib_route(prev)
+
+
 def _r(t):
     """round to bf16, back to fp32 CPU"""
     return t.to(BF).float().cpu()
@@ -156,6 +172,57 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     buf = C.create_string_buffer(128)
     _lib.lib().gvl_gemm_kernel_name(C.byref(d), buf, 128)
     return buf.value.decode()
+
+
+@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(16384, 768, 3072, 0, 1), (8064, 768, 2304, 0, 1),
+                                             (8064, 768, 768, 0, 0), (4096, 50304, 768, 0, 0)])
+def test_gemm_library_route(cuda, M, N, K, a_mn, b_mn):
+    """Plain GEMMs of the shapes measured faster on hipBLASLt (gemm_lib.cpp: the N = 768 dX
+    products, the lm_head forward) run there from inside gvl_gemm; fused ones never do.  vs
+    the fp32 product, with alpha, and replayed from a captured hipGraph."""
+    K_ = _k()
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="plain") == "hipblaslt"
+    assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="bias") != "hipblaslt"
+    ref = a.float() @ b.float()
+    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), alpha=0.5)
+    assert rel_err(y.float().cpu().numpy(), 0.5 * ref.numpy()) < 8e-3
+    out = torch.empty(M, N, dtype=BF, device=cuda)
+    K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=out)  # warm (plan built outside capture)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_library_route_layouts(cuda, a_mn, b_mn):
+    """Every operand layout and ragged sizes through the hipBLASLt route (mode 2: every plain
+    GEMM), including a strided output view."""
+    from gvl import _lib
+    K_ = _k()
+    prev = _lib.lib().gvl_gemm_lib_route(2)
+    try:
+        M, N, K = 1000, 776, 160
+        torch.manual_seed(a_mn * 2 + b_mn)
+        a = torch.randn(M, K).to(BF)
+        b = torch.randn(K, N).to(BF)
+        A = (a.t().contiguous() if a_mn else a).to(cuda)
+        B = (b if b_mn else b.t().contiguous()).to(cuda)
+        assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="plain") == "hipblaslt"
+        big = torch.full((M, N + 8), 7.0, dtype=BF, device=cuda)
+        K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=big[:, :N])
+        assert rel_err(big[:, :N].float().cpu().numpy(), (a.float() @ b.float()).numpy()) < 8e-3
+        assert torch.all(big[:, N:] == 7.0)
+    finally:
+        _lib.lib().gvl_gemm_lib_route(prev)
 
 
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])

@@ -83,5 +83,16 @@ r4i)  # which hipBLASLt kernels (macro tile, MFMA, depth) beat the persistent / 
     cat $O/diag_table_$M.txt
   done
   ;;
+r4j)  # plain N = 768 / lm_head GEMMs on hipBLASLt (gemm_lib.cpp): full suite, then A/B
+  suite
+  for c in 1 0; do GVL_GEMM_LIB=$c diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_lib${c}_16384.log
+    GVL_GEMM_LIB=$c diag base 8064 all all; mv $O/diag_base_8064_all.log $O/diag_lib${c}_8064.log; done
+  for w in qformer lm; do for c in 1 0 1 0; do
+    a="--workload qformer --steps 10 --warmup 3"; [ $w = lm ] && a="--steps 2 --warmup 1 --no-secondary"
+    GVL_GEMM_LIB=$c timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/${w}_l$c.json 2> $O/${w}_l$c.err
+    fatal $? bench_$w
+    echo "$w lib=$c $(python -c "import json;d=json.load(open('$O/${w}_l$c.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
