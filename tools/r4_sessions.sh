@@ -94,5 +94,10 @@ r4j)  # plain N = 768 / lm_head GEMMs on hipBLASLt (gemm_lib.cpp): full suite, t
     echo "$w lib=$c $(python -c "import json;d=json.load(open('$O/${w}_l$c.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done; done
   ;;
+r4k)  # PMC anatomy of the persistent GEMM vs hipBLASLt: wave waits, MFMA busy, LDS, L2 (tools/pmc_gemm.sh)
+  GVL_GEMM_LIB=0 bash tools/pmc_gemm.sh $S "16384 3072 768 0 0 3 -1 5 act" "16384 768 3072 0 1 3 -1 5 plain" \
+    "16384 768 3072 0 1 9 -1 5 plain" "16384 50304 768 0 0 3 3 5 plain" "16384 50304 768 0 0 9 -1 5 plain"; fatal $? pmc_gemm
+  python tools/pmc_summary.py gpurun_out/pmc_$S > $O/pmc_summary.txt; cat $O/pmc_summary.txt; cat gpurun_out/pmc_$S/times.log | grep -v amdgpu.ids
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
