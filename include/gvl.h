@@ -123,8 +123,8 @@ int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len);
  * by one through gvl_gemm): the bench attributes the batched weight-gradient launches too. */
 int gvl_gemm_batched_kernel_name(char* buf, int32_t len);
 /* ABI v8: plain GEMMs (no bias / activation / residual / dropout / gate / alpha_ptr, bf16 C)
- * of the shapes where hipBLASLt's kernel is measured faster (N = 768 with 768 <= K <= 4096 and
- * the lm_head forward, M >= 4096) run on hipBLASLt from inside gvl_gemm (impl 3, cfg -1);
+ * of the shapes where hipBLASLt's kernel is measured faster (N = 768 with 768 <= K <= 4096,
+ * M >= 4096) run on hipBLASLt from inside gvl_gemm (impl 3, cfg -1);
  * gvl_gemm_kernel_name reports "hipblaslt" for them.  mode 0 = never, 1 = those shapes
  * (default; env GVL_GEMM_LIB), 2 = every plain GEMM (tests).  Returns the previous mode. */
 int gvl_gemm_lib_route(int32_t mode);

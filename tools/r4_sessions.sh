@@ -83,7 +83,9 @@ r4i)  # which hipBLASLt kernels (macro tile, MFMA, depth) beat the persistent / 
     cat $O/diag_table_$M.txt
   done
   ;;
-r4j)  # plain N = 768 / lm_head GEMMs on hipBLASLt (gemm_lib.cpp): full suite, then A/B
+r4j)  # plain N = 768 GEMMs on hipBLASLt (gemm_lib.cpp): the route tests alone first, full suite, then A/B
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "library_route" --timeout 120 \
+    --timeout-method thread -p no:cacheprovider > $O/route.log 2>&1; rc=$?; tail -3 $O/route.log; fatal $rc route_tests
   suite
   for c in 1 0; do GVL_GEMM_LIB=$c diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_lib${c}_16384.log
     GVL_GEMM_LIB=$c diag base 8064 all all; mv $O/diag_base_8064_all.log $O/diag_lib${c}_8064.log; done
@@ -98,6 +100,17 @@ r4k)  # PMC anatomy of the persistent GEMM vs hipBLASLt: wave waits, MFMA busy, 
   GVL_GEMM_LIB=0 bash tools/pmc_gemm.sh $S "16384 3072 768 0 0 3 -1 5 act" "16384 768 3072 0 1 3 -1 5 plain" \
     "16384 768 3072 0 1 9 -1 5 plain" "16384 50304 768 0 0 3 3 5 plain" "16384 50304 768 0 0 9 -1 5 plain"; fatal $? pmc_gemm
   python tools/pmc_summary.py gpurun_out/pmc_$S > $O/pmc_summary.txt; cat $O/pmc_summary.txt; cat gpurun_out/pmc_$S/times.log | grep -v amdgpu.ids
+  ;;
+r4l)  # persistent GEMM ring depth: NS = 5 (three K-steps in flight) vs 4, alternated
+  for v in ns5 base ns5 base; do diag $v 16384 wide all; diag $v 8064 wide all; done
+  GVL_LIB=$LIBDIR/libgvl_ns5.so timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_ns5.log 2>&1; fatal $? wgrad; grep x12 $O/wgrad_ns5.log
+  timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_base.log 2>&1; fatal $? wgrad; grep x12 $O/wgrad_base.log
+  for w in lm qformer; do for v in ns5 base ns5 base; do
+    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
+    a="--workload qformer --steps 10 --warmup 3"; [ $w = lm ] && a="--steps 2 --warmup 1 --no-secondary"
+    GVL_LIB=$L timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/${w}_$v.json 2> $O/${w}_$v.err; fatal $? bench_$w
+    echo "$w $v $(python -c "import json;d=json.load(open('$O/${w}_$v.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
   ;;
 *) echo "unknown session $S"; exit 2;;
 esac
