@@ -99,6 +99,11 @@ r4j)  # plain N = 768 GEMMs on hipBLASLt (gemm_lib.cpp): the route tests alone f
 r4k)  # PMC anatomy of the persistent GEMM vs hipBLASLt: wave waits, MFMA busy, LDS, L2 (tools/pmc_gemm.sh)
   GVL_GEMM_LIB=0 bash tools/pmc_gemm.sh $S "16384 3072 768 0 0 3 -1 5 act" "16384 768 3072 0 1 3 -1 5 plain" \
     "16384 768 3072 0 1 9 -1 5 plain" "16384 50304 768 0 0 3 3 5 plain" "16384 50304 768 0 0 9 -1 5 plain"; fatal $? pmc_gemm
+  for pn in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+            "GRBM_GUI_ACTIVE GRBM_COUNT TCC_HIT_sum TCC_MISS_sum"; do
+    d=gpurun_out/pmc_$S/wgrad_${pn%% *}
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pn --output-format csv -d $d -o run -- python tools/wgrad_diag.py > $d.log 2>&1; fatal $? pmc_wgrad
+  done
   python tools/pmc_summary.py gpurun_out/pmc_$S > $O/pmc_summary.txt; cat $O/pmc_summary.txt; cat gpurun_out/pmc_$S/times.log | grep -v amdgpu.ids
   ;;
 r4l)  # persistent GEMM ring depth: NS = 5 (three K-steps in flight) vs 4, alternated
