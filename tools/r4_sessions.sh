@@ -106,8 +106,11 @@ r4k)  # PMC anatomy of the persistent GEMM vs hipBLASLt: wave waits, MFMA busy, 
   done
   python tools/pmc_summary.py gpurun_out/pmc_$S > $O/pmc_summary.txt; cat $O/pmc_summary.txt; cat gpurun_out/pmc_$S/times.log | grep -v amdgpu.ids
   ;;
-r4l)  # persistent GEMM ring depth: NS = 5 (three K-steps in flight) vs 4, alternated
+r4l)  # persistent GEMM ring depth: NS = 5 (three K-steps in flight) vs 4, alternated; the
+      # direct-A four-wave kernel forced onto the wide (K = 768) shapes (GVL_W4=2)
   for v in ns5 base ns5 base; do diag $v 16384 wide all; diag $v 8064 wide all; done
+  GVL_W4=2 diag base 16384 wide all; mv $O/diag_base_16384_wide.log $O/diag_w4_16384_wide.log
+  GVL_W4=2 diag base 8064 wide all; mv $O/diag_base_8064_wide.log $O/diag_w4_8064_wide.log
   GVL_LIB=$LIBDIR/libgvl_ns5.so timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_ns5.log 2>&1; fatal $? wgrad; grep x12 $O/wgrad_ns5.log
   timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_base.log 2>&1; fatal $? wgrad; grep x12 $O/wgrad_base.log
   for w in lm qformer; do for v in ns5 base ns5 base; do
