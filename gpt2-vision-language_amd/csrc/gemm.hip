@@ -209,6 +209,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.act = d->act; p.dact = d->dact; p.c_f32 = d->c_fp32;
   p.splits = 1;
   p.cnt = 0;
+  p.st_nt = 0;
   p.bn = 256;
   p.bm = 256;
   p.kper = d->k;
@@ -224,7 +225,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 11, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 12, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -233,6 +234,14 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12)) {
+    GemmP q;
+    fill_params(d, q);
+    if (gvl::gemm_w4x_plan(q, d->a_mn, env().cfg == 12)) {
+      snprintf(buf, len, "gemm_w4x_kernel<%d, false, %s, %d>", q.bm, tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+      return 0;
+    }
+  }
   if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_routed(d)) {
     snprintf(buf, len, "hipblaslt");
     return 0;
@@ -295,6 +304,11 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GemmP p;
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12) &&
+      gvl::gemm_w4x_try(p, d->a_mn, d->b_mn, env().cfg == 12, s)) {  // AGPR four-wave kernel
+    GVL_LAUNCH_CHECK("gvl_gemm(w4x)");
+    return 0;
+  }
   if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_try(d, s)) {  // plain GEMM on hipBLASLt
     GVL_LAUNCH_CHECK("gvl_gemm(hipblaslt)");
     return 0;
@@ -385,6 +399,12 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
     p.Ab[i] = static_cast<const bf16_t*>(d[i].a);
     p.Bb[i] = static_cast<const bf16_t*>(d[i].b);
     p.Cb[i] = d[i].c;
+  }
+  if (d[0].a_mn && d[0].b_mn && gvl::gemm_w4x_batched_try(p, gvl::as_stream(stream))) {
+    snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, true, true, %d>",
+             gvl::gemm_epi_kind(p));
+    GVL_LAUNCH_CHECK("gvl_gemm_batched(w4x)");
+    return 0;
   }
   if (gvl::gemm_pp3_plan(p, true) && p.splits == 1) {
     // tile shape for the whole batch (the plan sized it for one problem): 256 rows, 256 or

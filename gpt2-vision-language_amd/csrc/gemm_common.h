@@ -29,6 +29,7 @@ struct GemmP {
   int group;  // tile rows per L2 group (gemm_work_tile)
   int act, dact, c_f32, has_drop;
   int cnt;  // gemm_pp3_kernel: counted epilogue (set by its launcher, gemm_pp3.h CntEpi)
+  int st_nt;  // gemm_pp3_kernel counted epilogue: streaming (sc1 nt) stores for outputs past the MALL
   // split-K: `splits` workgroups per output tile, each over K range [s*kper, (s+1)*kper),
   // writing fp32 partials to ws[s][M][N]; gemm_splitk_reduce applies the epilogue.
   int splits;
@@ -218,6 +219,7 @@ struct EpiPre {
   static constexpr int XH = FULL ? FM : FM / 2;  // else half a tile at a time, in the epilogue
   uint2 x[KD::AUX ? XH : 1][KD::AUX ? FN : 1];
   uint64_t seed = 0;  // effective dropout seed (DROP), read with the bias, not per element
+  bool pre0 = false;  // the first half (fragment rows 0 .. XH-1) was fetched ahead of the epilogue
   GVL_DEV void load_bias(const GemmP& p, int64_t nw0, int lane) {
     if constexpr (KD::DROP) seed = seed_eff(p.seed, p.seed_ptr);
     if constexpr (KD::BIAS) {
@@ -328,7 +330,8 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
   for (int i = 0; i < FM; ++i) {
     const int64_t m = mw0 + i * 16 + (lane & 15);
     const bool mok = m < p.M;
-    if (EpiKind<EPI>::AUX && !FULL && i % EpiPre<FM, FN, EPI>::XH == 0) pre.load_aux(p, mw0, nw0, lane, i, res);
+    if (EpiKind<EPI>::AUX && !FULL && i % EpiPre<FM, FN, EPI>::XH == 0 && !(i == 0 && pre.pre0))
+      pre.load_aux(p, mw0, nw0, lane, i, res);
 #pragma unroll
     for (int j = 0; j + 1 < FN; j += 2) {
       const int64_t n0 = nw0 + j * 16 + 4 * q, n1 = n0 + 16;
@@ -503,4 +506,7 @@ bool gemm_w4d_ok(const GemmP& p);  // gemm_w4d.hip: direct-A variant for a w4-pl
 bool gemm_lib_routed(const gvl_gemm_desc* d);         // gemm_lib.cpp: plain GEMM for hipBLASLt
 bool gemm_lib_try(const gvl_gemm_desc* d, hipStream_t s);  // launched there (else false)
 int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s);
+bool gemm_w4x_plan(GemmP& p, int a_mn, bool force);  // gemm_w4x.hip: AGPR four-wave kernel
+bool gemm_w4x_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
+bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s);  // batched dW (a_mn, b_mn, C += AB)
 }  // namespace gvl

@@ -51,11 +51,14 @@ bool plain(const gvl_gemm_desc* d) {
 }
 
 // The shapes measured faster on hipBLASLt (see the header): N = 768 outputs with K in
-// [768, 4096] at M >= 4096.  (The lm_head forward, also faster there, is not routed: its
+// [768, 4096] at M >= 12288, K >= 3072 below (at M = 8064 the direct-A kernel is as fast or
+// faster for K = 768 / 2304: 17.5 vs 20.1 us, 36.5 vs 36.4, profiles/r4/pp3_epilogue_diag_r4a.txt).
+// The M = 16384 ones reach gvl_gemm's AGPR four-wave kernel first (gemm_w4x.hip), which runs
+// them as fast (profiles/r4/w4x_shapes_r4o.txt).  (The lm_head forward, also faster there, is not routed: its
 // first routed run hit an illegal address inside the library (session r4j) and the cause
 // is not established.)
 bool measured_faster(const gvl_gemm_desc* d) {
-  return d->m >= 4096 && d->n == 768 && d->k >= 768 && d->k <= 4096;
+  return d->m >= 4096 && d->n == 768 && d->k <= 4096 && (d->k >= 3072 || (d->m >= 12288 && d->k >= 768));
 }
 
 LibPlan build(hipblasLtHandle_t h, const gvl_gemm_desc* d) {

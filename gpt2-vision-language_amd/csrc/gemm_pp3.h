@@ -48,7 +48,10 @@ GVL_DEV void wait_vm_steps_x(int n) {
 // the range check, no branch), so every epilogue issues exactly CNT_S stores per wave and the
 // NS - 2 following waits count them; the bias row is copied to LDS at kernel start and read by
 // inline asm (with its own lgkmcnt wait) in the epilogue.
-constexpr uint32_t CNT_OOB = 0x7FFFFFF0u;  // voffset past any buffer: the store is dropped
+constexpr uint32_t CNT_OOB = 0x7FFFFFF0u;
+// cache-policy bits of the counted epilogue's stores: default, or sc1 nt (streaming) for
+// outputs past the MALL (GemmP::st_nt)
+constexpr int CNT_NT = 18;  // voffset past any buffer: the store is dropped
 template <int EPI>
 struct CntEpi {
   using KD = EpiKind<EPI>;
@@ -90,7 +93,7 @@ GVL_DEV void cnt_bias<4>(uint32_t a, uint2 (&bv)[4]) {
 }
 
 // The counted epilogue: gemm_epilogue16's math and lane pairing, buffer stores.
-template <int FM, int FN, int EPI>
+template <int FM, int FN, int EPI, int AUX>
 GVL_DEV void gemm_epilogue_cnt(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,
                                int64_t nw0, int lane, float alpha, uint32_t bias_lds,
                                __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rp) {
@@ -116,12 +119,12 @@ GVL_DEV void gemm_epilogue_cnt(const GemmP& p, const float4_t (&acc)[FM][FN], in
       const int64_t n = nw0 + 16 * (j + (q & 1)) + 8 * (q >> 1);
       const bool ok = mok && n < p.N;
       __builtin_amdgcn_raw_buffer_store_b128(cnt_u32x4{sx[0], sy[0], sx[1], sy[1]}, rc,
-                                             cnt_off(ok, (m * p.ldc + n) * 2), 0, 0);
+                                             cnt_off(ok, (m * p.ldc + n) * 2), 0, AUX);
       if constexpr (KD::ACT) {
         const auto hx = __builtin_amdgcn_permlane16_swap(pack2(h0[0], h0[1]), pack2(h1[0], h1[1]), false, false);
         const auto hy = __builtin_amdgcn_permlane16_swap(pack2(h0[2], h0[3]), pack2(h1[2], h1[3]), false, false);
         __builtin_amdgcn_raw_buffer_store_b128(cnt_u32x4{hx[0], hy[0], hx[1], hy[1]}, rp,
-                                               cnt_off(ok, (m * p.ldp + n) * 2), 0, 0);
+                                               cnt_off(ok, (m * p.ldp + n) * 2), 0, AUX);
       }
     }
     if constexpr (FN % 2 == 1) {
@@ -131,10 +134,10 @@ GVL_DEV void gemm_epilogue_cnt(const GemmP& p, const float4_t (&acc)[FM][FN], in
       gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, 1.f, bv[j], z, v0, h0);
       const bool ok = mok && n0 < p.N;
       __builtin_amdgcn_raw_buffer_store_b64(cnt_u32x2{pack2(v0[0], v0[1]), pack2(v0[2], v0[3])}, rc,
-                                            cnt_off(ok, (m * p.ldc + n0) * 2), 0, 0);
+                                            cnt_off(ok, (m * p.ldc + n0) * 2), 0, AUX);
       if constexpr (KD::ACT)
         __builtin_amdgcn_raw_buffer_store_b64(cnt_u32x2{pack2(h0[0], h0[1]), pack2(h0[2], h0[3])}, rp,
-                                              cnt_off(ok, (m * p.ldp + n0) * 2), 0, 0);
+                                              cnt_off(ok, (m * p.ldp + n0) * 2), 0, AUX);
     }
   }
 }
@@ -316,8 +319,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp3_kernel(GemmP p) {
           _Pragma("unroll") for (int j_ = 0; j_ < FN; ++j_)                                  \
             asm volatile("" ::"v"(acc[i_][j_]));                                             \
       } else if (CNT && cnt_on) {                                                            \
-        gemm_epilogue_cnt<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha,       \
-                                       bias_lds, rc_cnt, rp_cnt);                            \
+        if (p.st_nt)                                                                         \
+          gemm_epilogue_cnt<FM, FN, EPI, CNT_NT>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, \
+                                                 bias_lds, rc_cnt, rp_cnt);                  \
+        else                                                                                 \
+          gemm_epilogue_cnt<FM, FN, EPI, 0>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha,  \
+                                            bias_lds, rc_cnt, rp_cnt);                       \
         cnt_w = NS - 2;                                                                      \
       } else {                                                                               \
         gemm_epilogue16<FM, FN, EPI>(p, acc, cu_m0 + arow, cu_n0 + bcol, lane, alpha, pre, c_, \
@@ -423,6 +430,17 @@ int launch_pp3_bn(const GemmP& p0, hipStream_t s) {
           p.M * p.ldc * 2 <= (int64_t)CNT_OOB &&
           (!EpiKind<EPI>::ACT || (p.pre_out != nullptr && p.M * p.ldp * 2 <= (int64_t)CNT_OOB)) &&
           (!EpiKind<EPI>::BIAS || ((reinterpret_cast<uintptr_t>(p.bias) & 15) == 0 && p.N % 8 == 0));
+  // outputs far beyond the 256 MiB MALL (the LM's lm_head logits, 1.65 GB) are stored streaming
+  // (sc1 nt): lm_head 1316 -> 1222 us, LM step +0.5 % (921k -> 925k tokens/s, same box,
+  // alternated).  The caption step's 811 MB logits stay on the default policy: part of them is
+  // still in the MALL when the CE kernel reads them (Q-Former step 15.21k vs 15.10k images/s
+  // with nt); outputs that fit measured far slower (c_fc + GELU 64 -> 120 us in a loop that
+  // rewrites them).  profiles/r4/pp3_store_policy_r4n_r4s.txt; GVL_PP3_NT=0 off.
+  static const bool nt_env = [] {
+    const char* e = getenv("GVL_PP3_NT");
+    return !(e && e[0] == '0');
+  }();
+  p.st_nt = p.cnt && nt_env && p.M * p.ldc * 2 > (int64_t)1 << 30;
   const int lds = ring + (p.cnt ? (int)bias_bytes : 0);
   auto kern = gemm_pp3_kernel<NS, AMN, BMN, EPI, BN, BM>;
   static bool attr_set = false;

@@ -96,20 +96,21 @@ struct Step {
   }
 };
 
-// 192-wide operand slab of a 32-deep K-step for 8 waves (gemm_pp3_kernel with BN = 192):
-// 12 DMA pieces, so waves 0-3 issue two and waves 4-7 one (piece j = wave + 8 t, j < 12).
+// 192-wide operand slab of a 32-deep K-step (gemm_pp3_kernel with BN = 192: 8 waves, so
+// waves 0-3 issue two of the 12 DMA pieces and waves 4-7 one, piece j = wave + 8 t, j < 12;
+// gemm_w4x_kernel: 4 waves, three pieces each).
 //  * K-contiguous: [192 rows][32] 64-B rows, the Step image;
 //  * MN-contiguous: cols 0-127 as the Step [32][128] half (256-B rows, fT swizzle), cols
 //    128-191 as [32][64] 128-B rows at +8 KiB, chunk c of k-row kr at c ^ f2(kr) (conflict-free
 //    ds_read_b64_tr_b16 lane groups for the fragment pattern below).
 GVL_DEV int f2(int k) { return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1; }  // 128-B rows
 
-template <bool MN>
+template <bool MN, int NWV = 8>
 struct Step192 {
-  static constexpr int R = 192, NWV = 8;
+  static constexpr int R = 192;
   static constexpr int BYTES = R * KS * 2;
-  static constexpr int NINSTR = BYTES / 1024;  // 12
-  static constexpr int PER = 2;                // pieces of waves 0-3 (waves 4-7: 1)
+  static constexpr int NINSTR = BYTES / 1024;                // 12
+  static constexpr int PER = (NINSTR + NWV - 1) / NWV;      // 8 waves: 2 for waves 0-3, 1 for 4-7
   GVL_DEV static int64_t elem(int64_t ld, int64_t r0, int64_t k0, int j, int lane) {
     if (!MN) {
       const int row = 16 * j + (lane >> 2);

@@ -142,6 +142,20 @@ def test_gemm_gelu_derivative_epilogues(cuda, M, N, K, act):
     assert rel_err(z.float().cpu().numpy(), ref.numpy()) < 8e-3
 
 
+class _pp3_routing:
+    """gvl_gemm_tune(3, 11): default routing without the four-wave kernels (gemm_w4 and the
+    AGPR gemm_w4x, which takes the plain / bias + residual M = 16384, N = 768 shapes by
+    default), for the tests that pin the persistent kernel on such shapes."""
+
+    def __enter__(self):
+        from gvl import _lib
+        _lib.lib().gvl_gemm_tune(3, 11)
+
+    def __exit__(self, *exc):
+        from gvl import _lib
+        _lib.lib().gvl_gemm_tune(3, -1)
+
+
 def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     """Kernel gvl_gemm picks for this shape; `epi` (a test epilogue name) sets the
     descriptor's epilogue fields the way gvl.kernels.gemm does (the routing depends on it)."""
@@ -174,12 +188,11 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
-@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(16384, 768, 3072, 0, 1), (8064, 768, 2304, 0, 1),
-                                             (8064, 768, 768, 0, 0)])
+@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 4096, 0, 0)])
 def test_gemm_library_route(cuda, M, N, K, a_mn, b_mn):
-    """Plain GEMMs of the shapes measured faster on hipBLASLt (gemm_lib.cpp: the N = 768 dX
-    products) run there from inside gvl_gemm; fused ones never do.  vs
-    the fp32 product, with alpha, and replayed from a captured hipGraph."""
+    """Plain GEMMs of the shapes measured faster on hipBLASLt (gemm_lib.cpp: the caption
+    decoder's c_fc.dX) run there from inside gvl_gemm; fused ones never do.  vs the fp32
+    product, with alpha, and replayed from a captured hipGraph."""
     K_ = _k()
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K).to(BF)
@@ -225,6 +238,47 @@ def test_gemm_library_route_layouts(cuda, a_mn, b_mn):
         _lib.lib().gvl_gemm_lib_route(prev)
 
 
+@pytest.mark.parametrize("b_mn", [0, 1])
+@pytest.mark.parametrize("epi", ["plain", "bias_res"])
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (16384, 768, 768), (1000, 776, 160),
+                                   (4096, 2304, 96), (512, 768, 64), (16384, 3072, 768),
+                                   (8064, 768, 3072), (8064, 768, 768)])
+def test_gemm_w4x(cuda, b_mn, epi, M, N, K):
+    """Four-wave AGPR-accumulator kernel (gemm_w4x.hip), forced with gvl_gemm_tune(3, 12) (and
+    chosen by default for the LM's N = 768 shapes, checked by name):
+    256- and 128-row tiles (the latter below ~0.9 chip of 256-row tiles: M = 8064), both B
+    layouts, plain (alpha 0.5) and bias + residual epilogues, ragged M / N tiles, K of 2 and 3
+    steps (shorter than the ring), one and four tiles per CU; the output is a strided
+    view inside a sentinel-filled buffer (no store past the tile edges)."""
+    from gvl import _lib
+    K_ = _k()
+    torch.manual_seed(M + N + K + b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = a.to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    h = a.float() @ b.float()
+    _lib.lib().gvl_gemm_tune(3, 12)
+    try:
+        assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x_kernel")
+        big = torch.full((M + 3, N + 8), 7.0, dtype=BF, device=cuda)
+        out = big[:M, :N]
+        if epi == "plain":
+            K_.gemm(A, B, b_mn=bool(b_mn), out=out, alpha=0.5)
+            ref = 0.5 * h
+        else:
+            bias, res = torch.randn(N).to(BF), torch.randn(M, N).to(BF)
+            K_.gemm(A, B, b_mn=bool(b_mn), out=out, bias=bias.to(cuda), residual=res.to(cuda))
+            ref = h + bias.float() + res.float()
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+    if M == 16384 and N == 768:
+        assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x_kernel")
+    assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
+    assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
+
+
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])
 @pytest.mark.parametrize("M,N,K", [(8064, 3072, 768), (7999, 2240, 768), (16384, 768, 3072),
                                    (4096, 2304, 768), (2048, 50304, 768)])
@@ -241,7 +295,8 @@ def test_gemm_counted_epilogue(cuda, epi, M, N, K):
     a = torch.randn(M, K).to(BF)
     b = (torch.randn(K, N) * 0.05).to(BF)
     A, B = a.to(cuda), b.t().contiguous().to(cuda)
-    name = _kernel_name(A, B, 0, 0, M, N, K, epi={"bias_act_erf_d": "bias_act_d"}.get(epi, epi))
+    with _pp3_routing():
+        name = _kernel_name(A, B, 0, 0, M, N, K, epi={"bias_act_erf_d": "bias_act_d"}.get(epi, epi))
     assert name.startswith("gemm_pp3_kernel"), name
     bias = torch.randn(N).to(BF)
     h = a.float() @ b.float() + (0 if epi == "plain" else bias.float())
@@ -255,7 +310,8 @@ def test_gemm_counted_epilogue(cuda, epi, M, N, K):
         g.sum().backward()
         pre = torch.empty(M, N, dtype=BF, device=cuda)
         kw, ref = dict(bias=bias.to(cuda), act=4 if erf else 3, pre_out=pre), g.detach()
-    y = K_.gemm(A, B, **kw)
+    with _pp3_routing():
+        y = K_.gemm(A, B, **kw)
     assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
     if "pre_out" in kw:
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
@@ -269,6 +325,32 @@ def test_gemm_counted_epilogue(cuda, epi, M, N, K):
         assert torch.equal(big[:M, :N], y)
         if "pre_out" in kw:
             assert torch.all(pbig[M:] == 7.0) and torch.all(pbig[:, N:] == 7.0)
+
+
+@pytest.mark.parametrize("act", [0, 3])
+def test_gemm_counted_epilogue_streaming_stores(cuda, act):
+    """Outputs past 1 GiB (the LM's lm_head logits) take the counted epilogue's streaming (sc1 nt)
+    stores: 10800 x 50304 bf16 = 1.09 GB, plain and with the GELU side output (two streams),
+    ragged M, vs the fp32 product."""
+    K_ = _k()
+    M, N, K = 10800, 50304, 128
+    torch.manual_seed(act)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A, B = a.to(cuda), b.t().contiguous().to(cuda)
+    h = a.float() @ b.float()
+    if act:
+        bias = torch.randn(N).to(BF)
+        pre = torch.empty(M, N, dtype=BF, device=cuda)
+        y = K_.gemm(A, B, bias=bias.to(cuda), act=3, pre_out=pre)
+        x = (h + bias.float()).requires_grad_(True)
+        g = O.gelu_tanh(x)
+        g.sum().backward()
+        assert rel_err(y.float().cpu().numpy(), g.detach().numpy()) < 8e-3
+        assert rel_err(pre.float().cpu().numpy(), x.grad.numpy()) < 8e-3
+    else:
+        y = K_.gemm(A, B)
+        assert rel_err(y.float().cpu().numpy(), h.numpy()) < 8e-3
 
 
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
@@ -285,7 +367,8 @@ def test_gemm_tile192(cuda, a_mn, b_mn, epi, M, N, K):
     b = (torch.randn(K, N) * 0.1).to(BF)
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
-    assert ", 192, " in _kernel_name(A, B, a_mn, b_mn, M, N, K)  # 256- or 128-row tiles
+    with _pp3_routing():
+        assert ", 192, " in _kernel_name(A, B, a_mn, b_mn, M, N, K)  # 256- or 128-row tiles
     h = a.float() @ b.float()
     bias = torch.randn(N).to(BF)
     res = torch.randn(M, N).to(BF)
@@ -303,7 +386,8 @@ def test_gemm_tile192(cuda, a_mn, b_mn, epi, M, N, K):
         hx = hpre.float().requires_grad_(True)
         O.gelu_tanh(hx).sum().backward()
         kw, ref = dict(dact=1, pre_in=hpre.to(cuda)), h * hx.grad
-    y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
+    with _pp3_routing():
+        y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw)
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), (h + bias.float()).numpy()) < 8e-3
@@ -661,14 +745,21 @@ def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
 @pytest.mark.parametrize("count,M,N,K,acc", [(12, 768, 768, 4096, True), (12, 2304, 768, 2048, True),
                                              (3, 3072, 768, 1024, False), (2, 200, 136, 96, True),
                                              (17, 256, 256, 64, True), (12, 768, 768, 16384, True),
-                                             (12, 768, 768, 1024, False)])
+                                             (12, 768, 768, 1024, False), (12, 3072, 768, 1024, True),
+                                             (12, 768, 3072, 512, True), (12, 1000, 776, 96, True),
+                                             (9, 3072, 768, 256, True)])
 def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
     """gvl_gemm_batched: `count` weight-gradient GEMMs dW_i (+)= dY_i^T X_i (both operands
     MN-contiguous, as the deferred GPT-2 block weight gradients) in one persistent launch;
     each equals its own reference.  count 17 (> 16) and a ragged shape exercise the fallback.
     12 x (768, 768) — the LM's attn.c_proj at K = 16384 and shorter — runs as a two-way K
     split combined in-launch, with the fused bias row sums combined through the workspace;
-    the second (dbias) launch also checks that the first left the tickets at zero."""
+    the second (dbias) launch also checks that the first left the tickets at zero.  Batches of
+    accumulating problems whose 256 x 192 tiles fill the chip run on the AGPR four-wave kernel
+    (gemm_w4x.hip: MN-contiguous A and B by asm transposed reads, fused bias row sums), incl.
+    ragged M / N and a 3-step K."""
+    import ctypes as C
+    from gvl import _lib
     K_ = _k()
     torch.manual_seed(count + M + N + K)
     dys = [torch.randn(K, M).to(BF) for _ in range(count)]
@@ -677,6 +768,10 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
     outs = [c.to(cuda) for c in c0]
     K_.gemm_batched([(dy.to(cuda), x.to(cuda), o, acc) for dy, x, o in zip(dys, xs, outs)],
                     a_mn=True, b_mn=True)
+    buf = C.create_string_buffer(128)
+    _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
+    if acc and count == 12 and (M, N) in ((2304, 768), (1000, 776)):  # whole rounds of 256 x 192
+        assert buf.value.decode().startswith("gemm_w4x_kernel"), buf.value
     for dy, x, c, o in zip(dys, xs, c0, outs):
         ref = dy.float().t() @ x.float() + (c.float() if acc else 0)
         assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3

@@ -120,5 +120,84 @@ r4l)  # persistent GEMM ring depth: NS = 5 (three K-steps in flight) vs 4, alter
     echo "$w $v $(python -c "import json;d=json.load(open('$O/${w}_$v.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done; done
   ;;
+r4m)  # re-entry check of HEAD (hipBLASLt route on): route tests alone, GPU suite + smoke; persistent
+      # GEMM start stagger A/B (GVL_PP3_STAGGER, wide shapes + lm_head); step A/B of the route
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "library_route" --timeout 120 \
+    --timeout-method thread -p no:cacheprovider > $O/route.log 2>&1; rc=$?; tail -3 $O/route.log; fatal $rc route_tests
+  suite
+  for st in 0 6 12 0 6 12; do GVL_PP3_STAGGER=$st diag base 16384 wide epi; mv $O/diag_base_16384_wide.log $O/diag_st${st}_16384.log
+    GVL_PP3_STAGGER=$st diag base 8064 wide epi; mv $O/diag_base_8064_wide.log $O/diag_st${st}_8064.log; done
+  for w in qformer lm; do for c in 1 0 1 0; do
+    [ $w = lm ] && [ $c = 1 ] && [ -f $O/lm_l0.json ] && break
+    a="--workload qformer --steps 10 --warmup 3"; [ $w = lm ] && a="--steps 2 --warmup 1 --no-secondary"
+    GVL_GEMM_LIB=$c timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/${w}_l$c.json 2> $O/${w}_l$c.err
+    fatal $? bench_$w
+    echo "$w lib=$c $(python -c "import json;d=json.load(open('$O/${w}_l$c.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
+  ;;
+r4n)  # cache policy of the persistent GEMM's counted-epilogue stores (GVL_PP3_ST_AUX builds), alternated
+  for r in 1 2; do for v in base stnt stsc1 stsc1nt; do
+    diag $v 16384 wide epi; mv $O/diag_${v}_16384_wide.log $O/diag_${v}_16384_$r.log
+    diag $v 8064 wide epi; mv $O/diag_${v}_8064_wide.log $O/diag_${v}_8064_$r.log
+  done; done
+  ;;
+r4o)  # AGPR four-wave GEMM (gemm_w4x.hip): parity tests first, then shapes vs the defaults and hipBLASLt
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4x" --timeout 120 \
+    --timeout-method thread -p no:cacheprovider > $O/w4x_tests.log 2>&1; rc=$?; tail -3 $O/w4x_tests.log; fatal $rc w4x_tests
+  for r in 1 2; do
+    diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_def_16384n_$r.log
+    GVL_GEMM_CFG=12 diag base 16384 narrow all; mv $O/diag_base_16384_narrow.log $O/diag_w4x_16384n_$r.log
+  done
+  ;;
+r4p)  # LM step with the AGPR four-wave kernel on its N = 768 shapes (GVL_W4X=1) vs off, alternated
+  for x in 1 0 1 0; do
+    GVL_W4X=$x timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_x$x.json 2> $O/lm_x$x.err
+    fatal $? bench_lm
+    echo "lm w4x=$x $(python -c "import json;d=json.load(open('$O/lm_x$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:40],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:8]])")"
+  done
+  ;;
+r4q)  # head check with the AGPR four-wave kernel on by default + refined hipBLASLt route: GPU suite,
+      # smoke, the driver's default bench
+  suite
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],d['caption_qformer']['value'])"
+  ;;
+r4r)  # AGPR four-wave kernel: 128-row tiles on the caption decoder's N = 768 shapes (GVL_W4X_128) and
+      # the batched weight gradients (GVL_W4X_DW): parity tests, shapes, step A/B
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4x or library_route or batched_wgrad" \
+    --timeout 120 --timeout-method thread -p no:cacheprovider > $O/w4x_tests.log 2>&1; rc=$?; tail -3 $O/w4x_tests.log; fatal $rc w4x_tests
+  for r in 1 2; do
+    diag base 8064 narrow all; mv $O/diag_base_8064_narrow.log $O/diag_def_8064n_$r.log
+    GVL_W4X_128=1 diag base 8064 narrow all; mv $O/diag_base_8064_narrow.log $O/diag_x128_8064n_$r.log
+  done
+  for x in 1 0 1 0; do
+    GVL_W4X_DW=$x timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_dw$x.log 2>&1; fatal $? wgrad; echo "dw=$x"; grep x12 $O/wgrad_dw$x.log
+  done
+  for x in 1 0 1 0; do
+    GVL_W4X_128=$x timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf_x$x.json 2> $O/qf_x$x.err
+    fatal $? bench_qf
+    echo "qformer w4x128=$x $(python -c "import json;d=json.load(open('$O/qf_x$x.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done
+  for x in 1 0 1 0; do
+    GVL_W4X_DW=$x timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_dw$x.json 2> $O/lm_dw$x.err
+    fatal $? bench_lm
+    echo "lm w4x_dw=$x $(python -c "import json;d=json.load(open('$O/lm_dw$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:44],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:4]])")"
+  done
+  ;;
+r4s)  # streaming stores for outputs past the MALL (GVL_PP3_NT) + w4x batched dW on full-round batches:
+      # kernel tests, then LM step A/B of each
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4x or batched_wgrad or counted_epilogue or library_route" \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  for v in "1 1" "0 1" "1 0" "1 1" "0 1" "1 0"; do set -- $v
+    GVL_PP3_NT=$1 GVL_W4X_DW=$2 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_$1$2.json 2> $O/lm_$1$2.err
+    fatal $? bench_lm
+    echo "lm nt=$1 dw=$2 $(python -c "import json;d=json.load(open('$O/lm_$1$2.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:44],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
+  done
+  for v in 1 0 1 0; do
+    GVL_PP3_NT=$v timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf_nt$v.json 2> $O/qf_nt$v.err
+    fatal $? bench_qf
+    echo "qformer nt=$v $(python -c "import json;d=json.load(open('$O/qf_nt$v.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
