@@ -238,7 +238,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     GemmP q;
     fill_params(d, q);
     if (gvl::gemm_w4x_plan(q, d->a_mn, env().cfg == 12)) {
-      snprintf(buf, len, "gemm_w4x_kernel<%d, false, %s, %d>", q.bm, tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+      snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d>", q.bm, d->a_mn ? q.bn : 192, tf[d->a_mn != 0],
+               tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
       return 0;
     }
   }
@@ -401,7 +402,9 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
     p.Cb[i] = d[i].c;
   }
   if (d[0].a_mn && d[0].b_mn && gvl::gemm_w4x_batched_try(p, gvl::as_stream(stream))) {
-    snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, true, true, %d>",
+    GemmP q = p;
+    gvl::w4x_dw_plan(q);
+    snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, %d, true, true, %d>", q.bn,
              gvl::gemm_epi_kind(p));
     GVL_LAUNCH_CHECK("gvl_gemm_batched(w4x)");
     return 0;

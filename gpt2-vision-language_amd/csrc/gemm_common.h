@@ -509,4 +509,5 @@ int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s);
 bool gemm_w4x_plan(GemmP& p, int a_mn, bool force);  // gemm_w4x.hip: AGPR four-wave kernel
 bool gemm_w4x_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s);  // batched dW (a_mn, b_mn, C += AB)
+bool w4x_dw_plan(GemmP& p);  // its tile choice (bm / bn / tiles), false when not routed
 }  // namespace gvl

@@ -32,8 +32,7 @@ namespace {
 
 using namespace gvl_ring;
 
-constexpr int X_BN = 192, X_FN = 6;
-// ring slots by tile height: 5 x 28 KiB (256 rows), 7 x 20 KiB (128 rows)
+// ring slots by tile: 5 x 28 KiB (256 x 192), 7 x 20 KiB (128 x 192), 5 x 32 KiB (256 x 256)
 template <int BM>
 constexpr int x_ns() { return BM == 256 ? 5 : 7; }
 
@@ -54,13 +53,13 @@ constexpr int x_ns() { return BM == 256 ? 5 : 7; }
 // its result (24 wait states >= the XDL write -> VALU read / write requirement of a 16x16x32
 // MFMA) before any instruction below it reads or rewrites an accumulator, and a zeroing write
 // above it lands before an MFMA below reads it as srcC.
-template <int FM>
-GVL_DEV void w4x_fence(float4_t (&acc)[FM][X_FN]) {
+template <int FM, int FN>
+GVL_DEV void w4x_fence(float4_t (&acc)[FM][FN]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < X_FN; ++j) W4X_PIN(acc[i][j]);
+    for (int j = 0; j < FN; ++j) W4X_PIN(acc[i][j]);
 }
 
 // one 1-KiB LDS-DMA piece (a device function: target builtins in a __global__ body are host
@@ -95,11 +94,9 @@ GVL_DEV short8_t w4x_frag_bmn(const char* slab, int c0, int lane) {
   r.hi = hv;
   return r;
 }
-// lgkmcnt(0) with a step's 14 fragments threaded through: hipcc sees them redefined here, so
-// it adds no waits of its own for them further down the step (its count of LDS operations in
-// flight also misses the asm reads)
-// A fragment of an MN-contiguous slab (the Step<BM, true> image: [32][128] 256-B rows per
-// 128-row half, fT swizzle) by inline asm, for the weight gradients (A = dY^T): as w4x_frag_bmn.
+// Fragment of an MN-contiguous Step<R, true> slab ([32][128] 256-B rows per 128-row / column
+// half, fT swizzle) by inline asm: the A operand of the weight gradients (dY^T) and a 256-wide
+// MN-contiguous B; as w4x_frag_bmn.
 GVL_DEV short8_t w4x_frag_amn(const char* slab, int c0, int lane) {
   const int G = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
   const int kr = 8 * G + q;
@@ -116,10 +113,22 @@ GVL_DEV short8_t w4x_frag_amn(const char* slab, int c0, int lane) {
   return r;
 }
 
-template <int FM>
-GVL_DEV void w4x_wait(short8_t (&a)[FM], short8_t (&b)[X_FN]);
+// lgkmcnt(0) with a step's fragments threaded through: hipcc sees them redefined here, so it
+// adds no waits of its own for them further down the step (its count of LDS operations in
+// flight also misses the asm reads)
+template <int FM, int FN>
+GVL_DEV void w4x_wait(short8_t (&a)[FM], short8_t (&b)[FN]);
 template <>
-GVL_DEV void w4x_wait<8>(short8_t (&a)[8], short8_t (&b)[X_FN]) {
+GVL_DEV void w4x_wait<8, 8>(short8_t (&a)[8], short8_t (&b)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
+                 "+v"(a[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
+                 "+v"(b[6]), "+v"(b[7])
+               :
+               : "memory");
+}
+template <>
+GVL_DEV void w4x_wait<8, 6>(short8_t (&a)[8], short8_t (&b)[6]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
                  "+v"(a[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5])
@@ -127,7 +136,7 @@ GVL_DEV void w4x_wait<8>(short8_t (&a)[8], short8_t (&b)[X_FN]) {
                : "memory");
 }
 template <>
-GVL_DEV void w4x_wait<4>(short8_t (&a)[4], short8_t (&b)[X_FN]) {
+GVL_DEV void w4x_wait<4, 6>(short8_t (&a)[4], short8_t (&b)[6]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
                  "+v"(b[3]), "+v"(b[4]), "+v"(b[5])
@@ -135,21 +144,33 @@ GVL_DEV void w4x_wait<4>(short8_t (&a)[4], short8_t (&b)[X_FN]) {
                : "memory");
 }
 
-// BM = 256: waves 2 x 2 of 128 x 96; BM = 128 (the caption decoder's 8064 rows: 252 tiles of
-// 128 x 192 at N = 768): waves of 64 x 96 (4 x 6 fragments, 0.42 reads per MFMA).
-template <int BM, bool AMN, bool BMN, int EPI>
+// B slab of a BN-wide tile: the persistent kernel's 192-wide image, or the standard 256 one
+template <int BN, bool MN>
+struct XSlabB {
+  using type = Step192<MN, 4>;
+};
+template <bool MN>
+struct XSlabB<256, MN> {
+  using type = Step<256, MN, 4>;
+};
+
+// BM x BN = 256 x 192: waves 2 x 2 of 128 x 96 (8 x 6 fragments); 128 x 192 (the caption
+// decoder's 8064 rows: 252 tiles at N = 768): waves of 64 x 96 (0.42 reads per MFMA); 256 x 256:
+// waves of 128 x 128 (8 x 8 fragments = all 256 AGPRs, 0.25 reads per MFMA).
+template <int BM, int BN, bool AMN, bool BMN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
-  constexpr int NS = x_ns<BM>(), FM = BM / 32, FN = X_FN;
-  using SA = Step<BM, AMN, 4>;     // 16 / 8 pieces: 4 / 2 per wave
-  using SB = Step192<BMN, 4>;      // 12 pieces: 3 per wave
+  constexpr int NS = x_ns<BM>(), FM = BM / 32, FN = BN / 32;
+  using SA = Step<BM, AMN, 4>;                // 16 / 8 pieces: 4 / 2 per wave
+  using SB = typename XSlabB<BN, BMN>::type;  // 12 / 16 pieces: 3 / 4 per wave
   constexpr int SLOT = SA::BYTES + SB::BYTES;
   constexpr int PER = SA::PER + SB::PER;
-  static_assert(SA::PER * 4 == SA::NINSTR && SB::PER == 3, "piece split");
+  static_assert(SA::PER * 4 == SA::NINSTR && SB::PER * 4 == SB::NINSTR, "piece split");
+  static_assert(NS * SLOT <= 160 * 1024, "LDS");
   static_assert((NS - 2) * PER <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int arow = (wave >> 1) * (BM / 2), bcol = (wave & 1) * 96;
+  const int arow = (wave >> 1) * (BM / 2), bcol = (wave & 1) * (BN / 2);
   const int per_batch = p.tiles_m * p.tiles_n;
   const int total = per_batch * p.batch;
   const int G = gridDim.x;
@@ -183,7 +204,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     const int bi = work / per_batch;  // batch-major: a problem's tiles stay together
     int split, tm, tn;
     gemm_tile_of(work - bi * per_batch, 1, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
-    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * X_BN;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
     void* const cout = p.batch > 1 ? p.Cb[bi] : p.C;
     const bf16_t* const res = p.batch > 1 ? static_cast<const bf16_t*>(p.Cb[bi]) : p.residual;
     if (p.batch > 1) {
@@ -235,7 +256,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
       fa[0][i] = AMN ? w4x_frag_amn(smem, arow + 16 * i, lane) : SA::frag(smem, arow + 16 * i, lane);
 #pragma unroll
     for (int j = 0; j < FN; ++j)
-      fb[0][j] = BMN ? w4x_frag_bmn(smem + SA::BYTES, bcol + 16 * j, lane)
+      fb[0][j] = BMN ? (BN == 192 ? w4x_frag_bmn(smem + SA::BYTES, bcol + 16 * j, lane)
+                                  : w4x_frag_amn(smem + SA::BYTES, bcol + 16 * j, lane))
                      : SB::frag(smem + SA::BYTES, bcol + 16 * j, lane);
 
     // One K-step: its fragments (buffer CUR) landed, step c+1's slot published by the barrier,
@@ -261,9 +283,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
       if (nx_) {                                                                               \
         fa[NXT][i] = AMN ? w4x_frag_amn(sl_, arow + 16 * i, lane)                             \
                          : SA::frag(sl_, arow + 16 * i, lane);                                 \
-        /* B fragments i, i + FM, ..: FN = 6 > FM = 4 for 128-row tiles */                      \
+        /* B fragments i, i + FM, ..: FN > FM for 128-row tiles */                             \
         _Pragma("unroll") for (int j_ = i; j_ < FN; j_ += FM)                                  \
-          fb[NXT][j_] = BMN ? w4x_frag_bmn(sl_ + SA::BYTES, bcol + 16 * j_, lane)             \
+          fb[NXT][j_] = BMN ? (BN == 192 ? w4x_frag_bmn(sl_ + SA::BYTES, bcol + 16 * j_, lane) \
+                                         : w4x_frag_amn(sl_ + SA::BYTES, bcol + 16 * j_, lane)) \
                             : SB::frag(sl_ + SA::BYTES, bcol + 16 * j_, lane);                 \
       }                                                                                        \
       if (dm_) {                                                                               \
@@ -315,9 +338,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   }
 }
 
-template <int BM, bool AMN, bool BMN, int EPI>
+template <int BM, int BN, bool AMN, bool BMN, int EPI>
 void launch_w4x(const GemmP& p, hipStream_t s) {
-  auto kern = gemm_w4x_kernel<BM, AMN, BMN, EPI>;
+  auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -325,15 +348,15 @@ void launch_w4x(const GemmP& p, hipStream_t s) {
   }
   const int total = p.tiles_m * p.tiles_n * p.batch;
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
-  constexpr int lds = x_ns<BM>() * (BM + X_BN) * KS * 2;
+  constexpr int lds = x_ns<BM>() * (BM + BN) * KS * 2;
   gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
 }
 
 template <int BM, bool BMN>
 bool launch_w4x_epi(const GemmP& p, hipStream_t s) {
   switch (gvl::gemm_epi_kind(p)) {
-    case EPI_PLAIN: launch_w4x<BM, false, BMN, EPI_PLAIN>(p, s); return true;
-    case EPI_BIAS_RES: launch_w4x<BM, false, BMN, EPI_BIAS_RES>(p, s); return true;
+    case EPI_PLAIN: launch_w4x<BM, 192, false, BMN, EPI_PLAIN>(p, s); return true;
+    case EPI_BIAS_RES: launch_w4x<BM, 192, false, BMN, EPI_BIAS_RES>(p, s); return true;
     default: return false;
   }
 }
@@ -356,13 +379,16 @@ int w4x_mode() {
 // The kernel takes K-contiguous A (activations / dY), either B layout, bf16 out, K % 32 == 0,
 // plain or bias + residual epilogues, one problem, no split.  Routed: outputs whose 256 x 192
 // tiling fills the chip in whole rounds (M = 16384, N = 768: 256 tiles).
+bool w4x_dw_plan(GemmP& p);
+
 bool gemm_w4x_plan(GemmP& p, int a_mn, bool force) {
   const int epi = gemm_epi_kind(p);
-  if (a_mn || p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.N % 8 != 0 || p.ldc % 8 != 0 ||
+  if (a_mn) return p.batch == 1 && w4x_dw_plan(p) && p.K >= 4096;  // the lm_head's dW (b_mn)
+  if ( p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.N % 8 != 0 || p.ldc % 8 != 0 ||
       p.lda % 8 != 0 || p.ldb % 8 != 0 || (epi != EPI_PLAIN && epi != EPI_BIAS_RES))
     return false;
   // 256-row tiles where they (nearly) fill the chip, else 128-row tiles
-  const int64_t cus = num_cus(), tn = (p.N + X_BN - 1) / X_BN;
+  const int64_t cus = num_cus(), tn = (p.N + 192 - 1) / 192;
   p.bm = ((p.M + 255) / 256) * tn * 10 >= cus * 9 ? 256 : 128;
   p.tiles_m = (int)((p.M + p.bm - 1) / p.bm);
   p.tiles_n = (int)tn;
@@ -380,43 +406,56 @@ bool gemm_w4x_plan(GemmP& p, int a_mn, bool force) {
   return rows128 && p.N == 768 && tiles * 10 >= cus * 9 && tiles <= cus;
 }
 
+bool gemm_w4x_dw_try(const GemmP& p0, hipStream_t s);
+
 bool gemm_w4x_try(const GemmP& p0, int a_mn, int b_mn, bool force, hipStream_t s) {
   GemmP p = p0;
   if (!gemm_w4x_plan(p, a_mn, force)) return false;
+  if (a_mn) return b_mn && gemm_w4x_dw_try(p0, s);
   if (p.bm == 256) return b_mn ? launch_w4x_epi<256, true>(p, s) : launch_w4x_epi<256, false>(p, s);
   return b_mn ? launch_w4x_epi<128, true>(p, s) : launch_w4x_epi<128, false>(p, s);
 }
 
-// Batched weight gradients (gvl_gemm_batched[_dbias]: the 12 blocks' dW = dY^T X of one shape,
-// both operands MN-contiguous, C += AB, bias gradients fused): whole-K 256 x 192 tiles, when
-// the batch's tiles fill the chip in nearly whole rounds — the 12 attn.c_proj problems (144
-// tiles) keep the persistent kernel's in-launch K split.  GVL_W4X_DW=0 turns it off (A/B).
-bool gemm_w4x_batched_try(const GemmP& p0, hipStream_t s) {
+// Weight gradients (dW = dY^T X, both operands MN-contiguous, C += AB): the 12 blocks' of one
+// shape in one batched launch (gvl_gemm_batched[_dbias], bias gradients fused) or the tied
+// lm_head's alone (gvl_gemm), whole-K tiles of 256 x 192 or 256 x 256, whichever fills the last
+// round of CUs better (192 counted at 0.95: its per-wave block reads 0.29 vs 0.25 fragments per
+// MFMA), when that round is >= 65 % full: whole rounds matter more than the per-tile gain (12
+// c_attn problems, 432 tiles of 256 x 192 = two rounds, the last 69 % full: 785 vs 906 us on
+// the persistent kernel; 12 c_fc / mlp.c_proj ones as 576 such tiles, a third round 25 % full:
+// 1109 / 1014 vs 989 / 964, profiles/r4/w4x_r4r.txt — 256 x 256 gives them 432).  The 12
+// attn.c_proj problems (144 / 108 tiles) keep the persistent kernel's in-launch K split.
+// GVL_W4X_DW=0 turns it off (A/B).
+bool w4x_dw_plan(GemmP& p) {
   static const bool on = [] {
     const char* e = getenv("GVL_W4X_DW");
     return !(e && e[0] == '0');
   }();
   if (!on || w4x_mode() == 0) return false;
-  GemmP p = p0;
-  const int epi = gemm_epi_kind(p);
-  if (epi != EPI_RES || p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.M % 8 != 0 || p.N % 8 != 0 ||
-      p.ldc % 8 != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0)
+  if (gemm_epi_kind(p) != EPI_RES || p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.M % 8 != 0 ||
+      p.N % 8 != 0 || p.ldc % 8 != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0)
     return false;
-  const int64_t cus = num_cus();
+  const int64_t cus = num_cus(), tm = (p.M + 255) / 256;
+  auto fill = [&](int64_t tiles) { return (double)tiles / (double)(((tiles + cus - 1) / cus) * cus); };
+  const int64_t t192 = tm * ((p.N + 191) / 192) * p.batch, t256 = tm * ((p.N + 255) / 256) * p.batch;
+  const double f192 = 0.95 * fill(t192), f256 = fill(t256);
   p.bm = 256;
-  p.tiles_m = (int)((p.M + 255) / 256);
-  p.tiles_n = (int)((p.N + X_BN - 1) / X_BN);
+  p.bn = f256 >= f192 ? 256 : 192;
+  p.tiles_m = (int)tm;
+  p.tiles_n = (int)((p.N + p.bn - 1) / p.bn);
   p.splits = 1;
   p.kper = p.K;
-  // whole rounds matter more than the per-tile gain: the 12 c_attn problems (432 tiles: the last
-  // of two rounds 69 % full) run 785 vs 906 us on the persistent kernel's 256 x 192 tiles, the
-  // 12 c_fc / mlp.c_proj ones (576 tiles: a third round 25 % full) 1109 / 1014 vs 989 / 964
-  // (profiles/r4/w4x_r4r.txt) — so only batches whose last round is >= 65 % full
-  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n * p.batch;
-  const int64_t rounds = (tiles + cus - 1) / cus;
-  if (tiles * 10 < cus * 9 || (rounds * cus - tiles) * 100 > cus * 35) return false;
-  launch_w4x<256, true, true, EPI_RES>(p, s);
+  const int64_t tiles = (p.bn == 256 ? t256 : t192);
+  return tiles * 10 >= cus * 9 && (p.bn == 256 ? f256 : f192 / 0.95) >= 0.65;
+}
+
+bool gemm_w4x_dw_try(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  if (!w4x_dw_plan(p)) return false;
+  if (p.bn == 256) launch_w4x<256, 256, true, true, EPI_RES>(p, s);
+  else launch_w4x<256, 192, true, true, EPI_RES>(p, s);
   return true;
 }
+bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s) { return gemm_w4x_dw_try(p, s); }
 
 }  // namespace gvl

@@ -327,6 +327,26 @@ def test_gemm_counted_epilogue(cuda, epi, M, N, K):
             assert torch.all(pbig[M:] == 7.0) and torch.all(pbig[:, N:] == 7.0)
 
 
+@pytest.mark.parametrize("M,N,K,bn", [(50304, 768, 4096, 256), (16000, 768, 4096, 192)])
+def test_gemm_w4x_wgrad_single(cuda, M, N, K, bn):
+    """The tied lm_head's weight gradient through gvl_gemm (C += alpha * dY^T X, both operands
+    MN-contiguous, alpha from a device scalar) on the AGPR four-wave kernel: 256 x 256 tiles
+    at the vocabulary's 50304 rows (591 tiles), 256 x 192 where they fill the chip better."""
+    K_ = _k()
+    torch.manual_seed(M + K)
+    dy = (torch.randn(K, M) * 0.1).to(BF)
+    x = (torch.randn(K, N) * 0.1).to(BF)
+    c0 = torch.randn(M, N).to(BF)
+    A, B = dy.to(cuda), x.to(cuda)
+    out = c0.to(cuda)
+    name = _kernel_name(A, B, 1, 1, M, N, K, epi="res_inplace")
+    assert name.startswith(f"gemm_w4x_kernel<256, {bn}, true, true"), name
+    scale = torch.tensor([0.25], device=cuda)
+    K_.gemm(A, B, a_mn=True, b_mn=True, alpha_ptr=scale, out=out, residual=out)
+    ref = 0.25 * (dy.float().t() @ x.float()) + c0.float()
+    assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("act", [0, 3])
 def test_gemm_counted_epilogue_streaming_stores(cuda, act):
     """Outputs past 1 GiB (the LM's lm_head logits) take the counted epilogue's streaming (sc1 nt)

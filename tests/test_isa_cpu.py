@@ -43,9 +43,13 @@ def test_checker_models_counted_lgkmcnt():
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_attention_kernels_have_no_pending_lds_reads(tmp_path):
-    src = os.path.join(ROOT, "gpt2-vision-language_amd", "csrc", "attention.hip")
-    out = tmp_path / "attention.s"
+@pytest.mark.parametrize("unit", ["attention", "gemm_w4x"])
+def test_asm_lds_kernels_have_no_pending_lds_reads(tmp_path, unit):
+    """attention.hip and gemm_w4x.hip issue transposed LDS reads by inline asm (hipcc's own
+    builtin drains the LDS-DMA queue in front of each one): none of their kernels may read a
+    register such a read is still filling."""
+    src = os.path.join(ROOT, "gpt2-vision-language_amd", "csrc", unit + ".hip")
+    out = tmp_path / (unit + ".s")
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
                     "-Wno-unused-function", "-mllvm", "-pragma-unroll-threshold=1000000", src, "-o",
                     str(out)], check=True, capture_output=True, timeout=600)

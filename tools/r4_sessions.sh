@@ -199,5 +199,17 @@ r4s)  # streaming stores for outputs past the MALL (GVL_PP3_NT) + w4x batched dW
     echo "qformer nt=$v $(python -c "import json;d=json.load(open('$O/qf_nt$v.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done
   ;;
+r4t)  # 256 x 256 AGPR tiles for the weight gradients (batched c_fc / mlp.c_proj, lm_head dW): tests, wgrad A/B, LM A/B
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4x or batched_wgrad" \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  for x in 1 0; do
+    GVL_W4X_DW=$x timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_dw$x.log 2>&1; fatal $? wgrad; echo "dw=$x"; grep x12 $O/wgrad_dw$x.log | cut -c1-200
+  done
+  for x in 1 0 1 0; do
+    GVL_W4X_DW=$x timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_dw$x.json 2> $O/lm_dw$x.err
+    fatal $? bench_lm
+    echo "lm w4x_dw=$x $(python -c "import json;d=json.load(open('$O/lm_dw$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:48],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
