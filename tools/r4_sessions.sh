@@ -211,5 +211,23 @@ r4t)  # 256 x 256 AGPR tiles for the weight gradients (batched c_fc / mlp.c_proj
     echo "lm w4x_dw=$x $(python -c "import json;d=json.load(open('$O/lm_dw$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:48],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
   done
   ;;
+r4u)  # persistent AGPR four-wave kernel (gemm_w4p.hip) on the wide short-K shapes: parity tests, shapes, steps
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4p" \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  for r in 1 2; do for M in 16384 8064; do
+    diag base $M wide all; mv $O/diag_base_${M}_wide.log $O/diag_def_${M}_$r.log
+    GVL_GEMM_CFG=13 diag base $M wide epi; mv $O/diag_base_${M}_wide.log $O/diag_w4p_${M}_$r.log
+  done; done
+  for x in 1 0 1 0; do
+    GVL_W4P=$x timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_p$x.json 2> $O/lm_p$x.err
+    fatal $? bench_lm
+    echo "lm w4p=$x $(python -c "import json;d=json.load(open('$O/lm_p$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:40],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:8]])")"
+  done
+  for x in 1 0 1 0; do
+    GVL_W4P=$x timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf_p$x.json 2> $O/qf_p$x.err
+    fatal $? bench_qf
+    echo "qformer w4p=$x $(python -c "import json;d=json.load(open('$O/qf_p$x.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
