@@ -225,7 +225,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 }  // namespace
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 13, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 12, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -240,14 +240,6 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     if (gvl::gemm_w4x_plan(q, d->a_mn, env().cfg == 12)) {
       snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d>", q.bm, d->a_mn ? q.bn : 192, tf[d->a_mn != 0],
                tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
-      return 0;
-    }
-  }
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 13)) {
-    GemmP q;
-    fill_params(d, q);
-    if (gvl::gemm_w4p_plan(q, d->a_mn, env().cfg == 13)) {
-      snprintf(buf, len, "gemm_w4p_kernel<%s, %d>", tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
       return 0;
     }
   }
@@ -316,11 +308,6 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12) &&
       gvl::gemm_w4x_try(p, d->a_mn, d->b_mn, env().cfg == 12, s)) {  // AGPR four-wave kernel
     GVL_LAUNCH_CHECK("gvl_gemm(w4x)");
-    return 0;
-  }
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 13) &&
-      gvl::gemm_w4p_try(p, d->a_mn, d->b_mn, env().cfg == 13, s)) {  // persistent AGPR kernel
-    GVL_LAUNCH_CHECK("gvl_gemm(w4p)");
     return 0;
   }
   if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_try(d, s)) {  // plain GEMM on hipBLASLt

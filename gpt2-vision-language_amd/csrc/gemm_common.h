@@ -510,6 +510,4 @@ bool gemm_w4x_plan(GemmP& p, int a_mn, bool force);  // gemm_w4x.hip: AGPR four-
 bool gemm_w4x_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s);  // batched dW (a_mn, b_mn, C += AB)
 bool w4x_dw_plan(GemmP& p);  // its tile choice (bm / bn / tiles), false when not routed
-bool gemm_w4p_plan(GemmP& p, int a_mn, bool force);  // gemm_w4p.hip: persistent AGPR kernel
-bool gemm_w4p_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 }  // namespace gvl

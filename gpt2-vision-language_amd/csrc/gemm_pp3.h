@@ -92,15 +92,6 @@ GVL_DEV void cnt_bias<4>(uint32_t a, uint2 (&bv)[4]) {
                : "v"(a));
 }
 
-template <>
-GVL_DEV void cnt_bias<6>(uint32_t a, uint2 (&bv)[6]) {  // gemm_w4p_kernel (96 columns per wave)
-  asm volatile("ds_read_b64 %0, %6\n\tds_read_b64 %1, %6 offset:32\n\tds_read_b64 %2, %6 offset:64\n\t"
-               "ds_read_b64 %3, %6 offset:96\n\tds_read_b64 %4, %6 offset:128\n\t"
-               "ds_read_b64 %5, %6 offset:160\n\ts_waitcnt lgkmcnt(0)"
-               : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3]), "=&v"(bv[4]), "=&v"(bv[5])
-               : "v"(a));
-}
-
 // The counted epilogue: gemm_epilogue16's math and lane pairing, buffer stores.
 template <int FM, int FN, int EPI, int AUX>
 GVL_DEV void gemm_epilogue_cnt(const GemmP& p, const float4_t (&acc)[FM][FN], int64_t mw0,

@@ -327,53 +327,6 @@ def test_gemm_counted_epilogue(cuda, epi, M, N, K):
             assert torch.all(pbig[M:] == 7.0) and torch.all(pbig[:, N:] == 7.0)
 
 
-@pytest.mark.parametrize("b_mn", [0, 1])
-@pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])
-@pytest.mark.parametrize("M,N,K", [(16384, 3072, 768), (4000, 3080, 128), (8192, 3072, 64),
-                                   (2048, 50304, 768), (300, 392, 192)])
-def test_gemm_w4p(cuda, b_mn, epi, M, N, K):
-    """Persistent AGPR four-wave kernel (gemm_w4p.hip), forced with gvl_gemm_tune(3, 13): the
-    ring running across tiles (4 tiles per CU at 16384 x 3072, 8 at the lm_head width, tiles of
-    2 K-steps so the prologue spans two tiles), ragged M / N (a partial last column tile, rows
-    past M), both B layouts, every counted epilogue kind incl. the gelu' side output; output
-    is a strided view in a sentinel-filled buffer."""
-    from gvl import _lib
-    K_ = _k()
-    if epi != "plain" and N > 4096:
-        pytest.skip("lm_head carries no bias (the bias row must fit in LDS after the ring)")
-    torch.manual_seed(M + N + K + len(epi) + b_mn)
-    a = torch.randn(M, K).to(BF)
-    b = (torch.randn(K, N) * 0.05).to(BF)
-    A = a.to(cuda)
-    B = (b if b_mn else b.t().contiguous()).to(cuda)
-    bias = torch.randn(N).to(BF)
-    h = a.float() @ b.float() + (0 if epi == "plain" else bias.float())
-    big = torch.full((M + 2, N + 8), 7.0, dtype=BF, device=cuda)
-    out = big[:M, :N]
-    kw, ref = {}, h
-    if epi == "bias":
-        kw = dict(bias=bias.to(cuda))
-    elif epi != "plain":
-        erf = epi == "bias_act_erf_d"
-        x = h.clone().requires_grad_(True)
-        g = O.gelu_erf(x) if erf else O.gelu_tanh(x)
-        g.sum().backward()
-        pre = torch.empty(M, N, dtype=BF, device=cuda)
-        kw, ref = dict(bias=bias.to(cuda), act=4 if erf else 3, pre_out=pre), g.detach()
-    _lib.lib().gvl_gemm_tune(3, 13)
-    try:
-        assert _kernel_name(A, B, 0, b_mn, M, N, K,
-                            epi={"bias_act_erf_d": "bias_act_d"}.get(epi, epi)).startswith("gemm_w4p_kernel")
-        K_.gemm(A, B, b_mn=bool(b_mn), out=out, **kw)
-        torch.cuda.synchronize()
-    finally:
-        _lib.lib().gvl_gemm_tune(3, -1)
-    assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
-    if "pre_out" in kw:
-        assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
-    assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
-
-
 @pytest.mark.parametrize("M,N,K,bn", [(50304, 768, 4096, 256), (16000, 768, 4096, 192)])
 def test_gemm_w4x_wgrad_single(cuda, M, N, K, bn):
     """The tied lm_head's weight gradient through gvl_gemm (C += alpha * dY^T X, both operands
