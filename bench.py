@@ -303,6 +303,7 @@ def dominant_kernel(summary, workload="lm", steps=1):
                   frac=round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                   mfma_busy=pmc_record(workload, k).get("mfma_busy"),
                   clock_ghz=pmc_record(workload, k).get("clock_ghz"),
+                  mfma_rate_frac=pmc_record(workload, k).get("mfma_rate_frac"),
                   traffic=pmc_record(workload, k).get("hbm_bytes"))
              for k, v in top]
     return dict(kernel=name, bound="mfma", achieved=round(achieved, 1), peak=PEAK_BF16_TFLOPS,
@@ -310,6 +311,7 @@ def dominant_kernel(summary, workload="lm", steps=1):
                 traffic=pmc_traffic(workload, name), traffic_unit="bytes/launch",
                 mfma_busy=pmc_record(workload, name).get("mfma_busy"),
                 clock_ghz=pmc_record(workload, name).get("clock_ghz"),
+                mfma_rate_frac=pmc_record(workload, name).get("mfma_rate_frac"),
                 launches=s["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 avg_flop_per_launch=s["flops"] / s["launches"],
                 timing="hip events bound to the kernel dispatch (hipExtLaunchKernelGGL), "

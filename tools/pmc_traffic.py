@@ -66,7 +66,10 @@ def main(root):
     out = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                      "eager bench steps; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch; "
                      "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), "
-                     "clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel duration (third pass)",
+                     "clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel duration (third pass; over-reads on launches "
+                     "of <~100 us, whose GRBM window exceeds the dispatch), mfma_rate_frac = mfma_busy x "
+                     "clock / 2.4 GHz = MFMA-pipe cycles per dispatch-duration cycle at the 2.4 GHz peak "
+                     "clock (exact either way)",
            "workloads": {}}
     for wl in ("lm", "qf"):
         fe = load(os.path.join(root, f"{wl}_FETCH_SIZE"), "FETCH_SIZE")
@@ -82,6 +85,10 @@ def main(root):
             if k in mc:
                 ks[k]["mfma_busy"] = round(mc[k][0], 4)
                 ks[k]["clock_ghz"] = round(mc[k][1], 3)
+                # busy x clock = MFMA cycles / duration: exact, where the two factors are not for
+                # short launches (GRBM_GUI_ACTIVE spans a few us more than the dispatch: clocks
+                # above the 2.4 GHz peak on ~10-80 us kernels)
+                ks[k]["mfma_rate_frac"] = round(mc[k][0] * mc[k][1] / 2.4, 4)
         out["workloads"][wl] = dict(sorted(ks.items(), key=lambda kv: -kv[1]["hbm_bytes"] * kv[1]["launches"]))
     print(json.dumps(out, indent=1))
 

@@ -229,5 +229,15 @@ r4u)  # persistent AGPR four-wave kernel (gemm_w4p.hip) on the wide short-K shap
     echo "qformer w4p=$x $(python -c "import json;d=json.load(open('$O/qf_p$x.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done
   ;;
+r4v)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of both steps
+  suite
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],d['caption_qformer']['value'])"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  for w in qf lm; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -25 $O/${w}_table.txt; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
