@@ -55,6 +55,7 @@ def test_traffic_table_from_counter_csvs(tmp_path):
 def test_committed_traffic_covers_bench_dominant_kernels():
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         t = json.load(f)["workloads"]
-    # the dominant GEMMs of the round-3 bench lines (profiles/r3/bench_r3s2.json)
-    assert t["lm"]["gemm_pp3_kernel<4, false, true, 0, 192, 256>"]["hbm_bytes"] > 0
-    assert t["qf"]["gemm_w4d_kernel<true, 0>"]["hbm_bytes"] > 0
+    # the dominant GEMMs of the round-4 bench lines (profiles/r4/bench_r4v.json), with MFMA busy
+    # and the exact MFMA-rate fraction
+    for wl, name in (("lm", "gemm_w4x_kernel<256, 256, true, true, 6>"), ("qf", "gemm_w4d_kernel<false, 2>")):
+        assert t[wl][name]["hbm_bytes"] > 0 and 0 < t[wl][name]["mfma_rate_frac"] < 1
