@@ -112,8 +112,10 @@ int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t c
  * 1 = 256x128, 2 = 128x128, 3 = 256x256/5 slots, 4/5 = ping-pong, 6 = 64x128); impl 3:
  * cfg 3 forces the persistent kernel, 10 the four-wave narrow-output kernels (192x128 /
  * 128x128 tiles, direct-A where K % 384 == 0) where they apply, 11 = default routing without
- * them; other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase kernel) is
- * rejected. */
+ * them (and without the AGPR four-wave kernel), 12 (ABI v8, round 4) the AGPR four-wave kernel
+ * (gemm_w4x.hip: 256 x 192 / 128 x 192 tiles, K-contiguous A, plain or bias + residual) where
+ * it applies; other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase
+ * kernel) is rejected. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
  * caller attribute event timings to the rocprofv3 kernel-trace rows). */
