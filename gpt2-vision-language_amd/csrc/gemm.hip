@@ -220,6 +220,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.tickets = d->tickets;
   p.nticket = d->tickets ? d->ticket_count : 0;
   p.batch = 1;
+  p.grouped = 0;
 }
 
 }  // namespace
@@ -238,8 +239,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     GemmP q;
     fill_params(d, q);
     if (gvl::gemm_w4x_plan(q, d->a_mn, env().cfg == 12)) {
-      snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d>", q.bm, d->a_mn ? q.bn : 192, tf[d->a_mn != 0],
-               tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+      snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d, false>", q.bm, d->a_mn ? q.bn : 192,
+               tf[d->a_mn != 0], tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
       return 0;
     }
   }
@@ -404,8 +405,8 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
   if (d[0].a_mn && d[0].b_mn && gvl::gemm_w4x_batched_try(p, gvl::as_stream(stream))) {
     GemmP q = p;
     gvl::w4x_dw_plan(q);
-    snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, %d, true, true, %d>", q.bn,
-             gvl::gemm_epi_kind(p));
+    snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, %d, true, true, %d, false>",
+             q.bn, gvl::gemm_epi_kind(p));
     GVL_LAUNCH_CHECK("gvl_gemm_batched(w4x)");
     return 0;
   }
@@ -489,6 +490,44 @@ static int gemm_batched_impl(const gvl_gemm_desc* d, void* const* dbias, int32_t
 
 extern "C" int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream) {
   return gemm_batched_impl(d, nullptr, count, stream);
+}
+
+// Grouped weight gradients (ABI v9): count problems of possibly different shapes, each
+// dW_i += dY_i^T X_i (a_mn = b_mn = 1, residual == c, same alpha), dbias[i] (may be null) +=
+// column sums of dY_i, in one launch of the AGPR four-wave kernel.  0: launched; -1: the
+// problems do not qualify, nothing launched (the caller runs them another way).
+extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
+                                gvl_stream_t stream) {
+  g_batched_name[0] = 0;
+  GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_grouped: bad arguments");
+  if (count > GVL_MAX_BATCH || env().impl < 3 || env().cfg >= 0) return -1;
+  for (int i = 0; i < count; ++i) {
+    const gvl_gemm_desc& e = d[i];
+    if (!(e.a_mn && e.b_mn && e.residual == e.c && e.ldr == e.ldc && e.alpha == d[0].alpha &&
+          !e.alpha_ptr && !e.bias && !e.act && !e.dact && !e.gate && e.drop_p == 0.f && !e.c_fp32 &&
+          e.m > 0 && e.n > 0 && e.k > 0 && gvl::aligned16(e.a) && gvl::aligned16(e.b) &&
+          gvl::aligned16(e.c)))
+      return -1;
+  }
+  GemmP p;
+  fill_params(&d[0], p);
+  p.ws = nullptr;
+  p.ws_bytes = 0;
+  p.tickets = nullptr;
+  p.nticket = 0;
+  p.batch = count;
+  for (int i = 0; i < GVL_MAX_BATCH; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
+  for (int i = 0; i < count; ++i) {
+    p.Ab[i] = static_cast<const bf16_t*>(d[i].a);
+    p.Bb[i] = static_cast<const bf16_t*>(d[i].b);
+    p.Cb[i] = d[i].c;
+    p.Mb[i] = d[i].m, p.Nb[i] = d[i].n, p.Kb[i] = d[i].k;
+    p.ldab[i] = d[i].lda, p.ldbb[i] = d[i].ldb, p.ldcb[i] = d[i].ldc;
+  }
+  if (!gvl::gemm_w4x_grouped_try(p, gvl::as_stream(stream))) return -1;
+  snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, 256, true, true, %d, true>", EPI_RES);
+  GVL_LAUNCH_CHECK("gvl_gemm_grouped");
+  return 0;
 }
 
 extern "C" int gvl_gemm_batched_kernel_name(char* buf, int32_t len) {

@@ -50,6 +50,12 @@ struct GemmP {
   // nn.Linear bias grad next to its weight grad dW = dY^T X: A = dY^T), computed by the
   // weight-gradient tiles of the first column block with MFMAs against a ones fragment
   void* Db[GVL_MAX_BATCH];
+  // grouped launch (gvl_gemm_grouped, gemm_w4x_kernel GR): problems of different sizes, the
+  // per-problem sizes / strides here, gtile[i] = problem i's first work item (gtile[batch] = all)
+  int grouped;
+  int64_t Mb[GVL_MAX_BATCH], Nb[GVL_MAX_BATCH], Kb[GVL_MAX_BATCH];
+  int64_t ldab[GVL_MAX_BATCH], ldbb[GVL_MAX_BATCH], ldcb[GVL_MAX_BATCH];
+  int gtile[GVL_MAX_BATCH + 1];
 };
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
@@ -510,4 +516,5 @@ bool gemm_w4x_plan(GemmP& p, int a_mn, bool force);  // gemm_w4x.hip: AGPR four-
 bool gemm_w4x_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s);  // batched dW (a_mn, b_mn, C += AB)
 bool w4x_dw_plan(GemmP& p);  // its tile choice (bm / bn / tiles), false when not routed
+bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s);  // grouped dW of different shapes
 }  // namespace gvl

@@ -157,7 +157,9 @@ struct XSlabB<256, MN> {
 // BM x BN = 256 x 192: waves 2 x 2 of 128 x 96 (8 x 6 fragments); 128 x 192 (the caption
 // decoder's 8064 rows: 252 tiles at N = 768): waves of 64 x 96 (0.42 reads per MFMA); 256 x 256:
 // waves of 128 x 128 (8 x 8 fragments = all 256 AGPRs, 0.25 reads per MFMA).
-template <int BM, int BN, bool AMN, bool BMN, int EPI>
+// GR: a grouped launch (gvl_gemm_grouped): the problems differ in M, N, K and strides
+// (GemmP::Mb.. / gtile), read per tile.
+template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   constexpr int NS = x_ns<BM>(), FM = BM / 32, FN = BN / 32;
   using SA = Step<BM, AMN, 4>;                // 16 / 8 pieces: 4 / 2 per wave
@@ -172,12 +174,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int arow = (wave >> 1) * (BM / 2), bcol = (wave & 1) * (BN / 2);
   const int per_batch = p.tiles_m * p.tiles_n;
-  const int total = per_batch * p.batch;
+  const int total = GR ? p.gtile[p.batch] : per_batch * p.batch;
   const int G = gridDim.x;
-  const int nks = (int)(p.K / KS);
-  const int64_t a_rows = AMN ? p.K : p.M, b_rows = BMN ? p.K : p.N;
-  __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, a_rows * p.lda * 2);
-  __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, b_rows * p.ldb * 2);
+  __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, (AMN ? p.K : p.M) * p.lda * 2);
+  __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B, (BMN ? p.K : p.N) * p.ldb * 2);
   // fused bias gradients of a batched weight-gradient launch (GemmP::Db, as gemm_pp3_kernel):
   // the tiles of column block 0 also sum their A fragments over K by MFMAs against a ones
   // fragment, each wave of a row half 4 of its 8 row fragments.  These accumulators are left
@@ -188,7 +188,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   short8_t ones;
 #pragma unroll
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
-  const int sa_step = SA::step_bytes(p.lda), sb_step = SB::step_bytes(p.ldb);
   // alpha x *alpha_ptr read once, before any DMA is in flight
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
@@ -201,20 +200,36 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     // XCD-contiguous remap of the virtual grid, then the L2-grouped walk (gemm_tile_of)
     const int q8 = total >> 3, r8 = total & 7, xcd = vid & 7;
     const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vid >> 3);
-    const int bi = work / per_batch;  // batch-major: a problem's tiles stay together
+    // this tile's problem (batch-major: a problem's tiles stay together) and its sizes
+    int bi, local, tiles_m = p.tiles_m, tiles_n = p.tiles_n;
+    int64_t M_ = p.M, N_ = p.N, K_ = p.K, lda_ = p.lda, ldb_ = p.ldb, ldc_ = p.ldc;
+    if constexpr (GR) {
+      bi = 0;
+      while (bi + 1 < p.batch && work >= p.gtile[bi + 1]) ++bi;
+      local = work - p.gtile[bi];
+      M_ = p.Mb[bi], N_ = p.Nb[bi], K_ = p.Kb[bi], lda_ = p.ldab[bi], ldb_ = p.ldbb[bi], ldc_ = p.ldcb[bi];
+      tiles_m = (int)((M_ + BM - 1) / BM);
+      tiles_n = (int)((N_ + BN - 1) / BN);
+    } else {
+      bi = work / per_batch;
+      local = work - bi * per_batch;
+    }
+    const int nks = (int)(K_ / KS);
+    const int64_t a_rows = AMN ? K_ : M_, b_rows = BMN ? K_ : N_;
+    const int sa_step = SA::step_bytes(lda_), sb_step = SB::step_bytes(ldb_);
     int split, tm, tn;
-    gemm_tile_of(work - bi * per_batch, 1, p.tiles_m, p.tiles_n, p.group, split, tm, tn);
+    gemm_tile_of(local, 1, tiles_m, tiles_n, p.group, split, tm, tn);
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
     void* const cout = p.batch > 1 ? p.Cb[bi] : p.C;
     const bf16_t* const res = p.batch > 1 ? static_cast<const bf16_t*>(p.Cb[bi]) : p.residual;
     if (p.batch > 1) {
-      ra = uniform_rsrc(p.Ab[bi], a_rows * p.lda * 2);
-      rb = uniform_rsrc(p.Bb[bi], b_rows * p.ldb * 2);
+      ra = uniform_rsrc(p.Ab[bi], a_rows * lda_ * 2);
+      rb = uniform_rsrc(p.Bb[bi], b_rows * ldb_ * 2);
     }
     bool do_db = false;
     if constexpr (DB) do_db = p.batch > 1 && n0 == 0 && p.Db[bi] != nullptr;
-    SA::base_offsets(p.lda, m0, 0, wave, lane, offa);
-    SB::base_offsets(p.ldb, n0, 0, wave, lane, offb);
+    SA::base_offsets(lda_, m0, 0, wave, lane, offa);
+    SB::base_offsets(ldb_, n0, 0, wave, lane, offb);
     // the first half of the epilogue operand (residual) is fetched two K-steps before the tile
     // ends (at the epilogue its latency is exposed: one tile per CU on the routed shapes); the
     // whole of it would spill
@@ -324,29 +339,35 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     w4x_fence(acc);
     // every wave is past its last fragment read of this tile before anyone's next prologue DMA
     __builtin_amdgcn_s_barrier();
-    gemm_epilogue16<FM, FN, EPI>(p, acc, m0 + arow, n0 + bcol, lane, alpha, pre, cout, res);
+    if constexpr (GR) {  // this problem's sizes for the epilogue (only the scalars used survive)
+      GemmP q = p;
+      q.M = M_, q.N = N_, q.ldc = ldc_, q.ldr = ldc_;
+      gemm_epilogue16<FM, FN, EPI>(q, acc, m0 + arow, n0 + bcol, lane, alpha, pre, cout, res);
+    } else {
+      gemm_epilogue16<FM, FN, EPI>(p, acc, m0 + arow, n0 + bcol, lane, alpha, pre, cout, res);
+    }
     if constexpr (DB) {
       if (do_db && (lane >> 4) == 0) {
         bf16_t* db_ = static_cast<bf16_t*>(p.Db[bi]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int64_t m_ = m0 + arow + 16 * ((wave & 1) * 4 + k) + lane;
-          if (m_ < p.M) db_[m_] = f2bf(bf2f(db_[m_]) + bacc[k][0] * alpha);
+          if (m_ < M_) db_[m_] = f2bf(bf2f(db_[m_]) + bacc[k][0] * alpha);
         }
       }
     }
   }
 }
 
-template <int BM, int BN, bool AMN, bool BMN, int EPI>
+template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false>
 void launch_w4x(const GemmP& p, hipStream_t s) {
-  auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI>;
+  auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI, GR>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  const int total = p.tiles_m * p.tiles_n * p.batch;
+  const int total = GR ? p.gtile[p.batch] : p.tiles_m * p.tiles_n * p.batch;
   const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
   constexpr int lds = x_ns<BM>() * (BM + BN) * KS * 2;
   gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
@@ -457,5 +478,33 @@ bool gemm_w4x_dw_try(const GemmP& p0, hipStream_t s) {
   return true;
 }
 bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s) { return gemm_w4x_dw_try(p, s); }
+
+// Weight gradients of different shapes in one launch (gvl_gemm_grouped: the Q-Former bridge's
+// deferred dW of one backward, 2-16 problems of 768 x 768 .. 3072 x 768 at K = 4096 tokens,
+// bias sums fused): whole-K 256 x 256 tiles, the problems' tile lists concatenated (GemmP::gtile);
+// each problem alone would be 9-36 tiles and a split-K launch + reduce + a column-sum pair.
+// p: batch, Ab / Bb / Cb / Db and the per-problem sizes set by the caller.  GVL_W4X_GR=0 off.
+bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = getenv("GVL_W4X_GR");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || w4x_mode() == 0 || p.batch < 1 || p.batch > GVL_MAX_BATCH) return false;
+  int t = 0;
+  for (int i = 0; i < p.batch; ++i) {
+    if (p.Kb[i] % KS != 0 || p.Kb[i] < 2 * KS || p.Mb[i] % 8 != 0 || p.Nb[i] % 8 != 0 ||
+        p.ldab[i] % 8 != 0 || p.ldbb[i] % 8 != 0 || p.ldcb[i] % 8 != 0)
+      return false;
+    p.gtile[i] = t;
+    t += (int)(((p.Mb[i] + 255) / 256) * ((p.Nb[i] + 255) / 256));
+  }
+  p.gtile[p.batch] = t;
+  p.grouped = 1;
+  p.bm = 256;
+  p.bn = 256;
+  p.splits = 1;
+  launch_w4x<256, 256, true, true, EPI_RES, true>(p, s);
+  return true;
+}
 
 }  // namespace gvl

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 8  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 9  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -72,6 +72,7 @@ SIGNATURES = {
     "gvl_gemm": (C.c_int, [C.POINTER(GemmDesc), c_vp]),
     "gvl_gemm_batched": (C.c_int, [C.POINTER(GemmDesc), c_i32, c_vp]),
     "gvl_gemm_batched_dbias": (C.c_int, [C.POINTER(GemmDesc), C.POINTER(c_vp), c_i32, c_vp]),
+    "gvl_gemm_grouped": (C.c_int, [C.POINTER(GemmDesc), C.POINTER(c_vp), c_i32, c_vp]),
     "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
     "gvl_gemm_kernel_name": (C.c_int, [C.POINTER(GemmDesc), C.c_char_p, c_i32]),
     "gvl_gemm_batched_kernel_name": (C.c_int, [C.c_char_p, c_i32]),

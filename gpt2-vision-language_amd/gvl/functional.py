@@ -118,10 +118,15 @@ _READY_HOOKS = []
 # micro-step's 16k tokens) are 9-36 output tiles each — alone they need a K split with fp32
 # slabs and a reduce kernel to fill the chip, batched they fill it with whole-K tiles; the 48
 # bias column sums (96 small launches) become 4 launch pairs (gvl_colsum_batched).
-# Only the per-block units repeated 12 times defer (GPTBlockFn, CrossAttnFn); the two-layer
-# Q-Former / linear bridge launch theirs in place (measured: deferring them is 0.5 % slower).
-# GVL_DEFER_WGRAD=0 launches each one in place.
+# The per-block units repeated 12 times defer (GPTBlockFn, CrossAttnFn) and are flushed as
+# batched launches per shape.  The bridge units (MLPFn, MHAFn's out_proj, LinearFn) defer too
+# (GVL_DEFER_BRIDGE, round 4): their few problems of different shapes are flushed as ONE grouped
+# launch (gvl_gemm_grouped) with the bias sums fused, instead of one split-K launch + reduce +
+# column-sum pair each (round 2 measured plain deferral of the bridge 0.5 % slower: per-shape
+# batches of 2 problems underfill the chip).  GVL_DEFER_WGRAD=0 launches each one in place.
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
+DEFER_BRIDGE = os.environ.get("GVL_DEFER_BRIDGE", "1") != "0"
+GROUPED_WGRAD = os.environ.get("GVL_GROUPED_WGRAD", "1") != "0"
 # Queue entries are tagged with the autograd graph task that produced them, and every task
 # that defers queues its OWN end-of-backward flush, which runs only that task's entries: two
 # backward passes (two models, two threads, a nested reentrant backward) never consume each
@@ -201,6 +206,8 @@ def flush_wgrads(task=None):
         key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
                dy2.device, st)
         groups.setdefault(key, []).append((p, g, dy2, x2))
+    if GROUPED_WGRAD and len(groups) >= 2:
+        groups = _flush_grouped(groups, paired)
     order = list(groups.items())
     ready = []
     for key, items in order:
@@ -237,6 +244,29 @@ def flush_wgrads(task=None):
                                      accumulate=True)
                     for p, *_ in chunk:
                         _ready(p)
+
+
+def _flush_grouped(groups, paired):
+    """Every queued weight gradient of the flush as one grouped launch when they share a stream,
+    number at most 16 and run over at most 8192 tokens (the bridge's; the LM blocks' K = 16384
+    batches stay per shape); returns the groups left to the per-shape path."""
+    items = [it for its in groups.values() for it in its]
+    if len({key[-1] for key in groups}) != 1 or len(items) > 16 or any(it[2].shape[0] > 8192 for it in items):
+        return groups
+    bias = [paired.pop(_dkey(d), None) for _, _, d, _ in items]
+    with torch.cuda.stream(next(iter(groups))[-1]):
+        ok = K.gemm_grouped([(dy2, x2, g) for _, g, dy2, x2 in items],
+                            dbias=[b[1] if b is not None else None for b in bias])
+    if not ok:
+        for (_, _, d, _), b in zip(items, bias):
+            if b is not None:
+                paired[_dkey(d)] = b
+        return groups
+    for (p, _, _, _), b in zip(items, bias):
+        _ready(p)
+        if b is not None:
+            _ready(b[0])
+    return {}
 
 
 def _final_flush(task):
@@ -563,8 +593,8 @@ class LinearFn(torch.autograd.Function):
         if drop_p > 0:
             dbr = K.dropout_mask_apply(dbr, drop_p, seed, seed_ptr=_off(dbr, drop_p))
         dx = K.linear_dx(dbr, w).view(shp) if _need(ctx, 0) else None
-        dw = _wgrad(ctx, 1, ctx.params[0], dbr, x2)
-        db = _bgrad(ctx, 2, ctx.params[1], dbr)
+        dw = _wgrad(ctx, 1, ctx.params[0], dbr, x2, defer=DEFER_BRIDGE)
+        db = _bgrad(ctx, 2, ctx.params[1], dbr, defer=DEFER_BRIDGE)
         return dx, dw, db, dres, dgate, None, None
 
 
@@ -596,11 +626,11 @@ class MLPFn(torch.autograd.Function):
         if drop_p > 0:
             d2 = K.dropout_mask_apply(d2, drop_p, seed, seed_ptr=_off(d2, drop_p))
         P = ctx.params
-        dw2 = _wgrad(ctx, 3, P[3], d2, h)
-        db2 = _bgrad(ctx, 4, P[4], d2)
+        dw2 = _wgrad(ctx, 3, P[3], d2, h, defer=DEFER_BRIDGE)
+        db2 = _bgrad(ctx, 4, P[4], d2, defer=DEFER_BRIDGE)
         dpre = K.linear_dx(d2, w2, dact=3 if GELU_DERIV else act, pre_in=hpre)
-        dw1 = _wgrad(ctx, 1, P[1], dpre, x2)
-        db1 = _bgrad(ctx, 2, P[2], dpre)
+        dw1 = _wgrad(ctx, 1, P[1], dpre, x2, defer=DEFER_BRIDGE)
+        db1 = _bgrad(ctx, 2, P[2], dpre, defer=DEFER_BRIDGE)
         dx = K.linear_dx(dpre, w1).view(shp) if _need(ctx, 0) else None
         return dx, dw1, db1, dw2, db2, dres, None, None, None
 
@@ -657,8 +687,8 @@ class MHAFn(torch.autograd.Function):
         dbr = (K.dropout_mask_apply(d2, p_out, seed, seed_ptr=_off(d2, p_out)) if p_out > 0
                else d2)
         P_in_w, P_in_b, P_out_w, P_out_b = ctx.params
-        d_out_w = _wgrad(ctx, 4, P_out_w, dbr, o.view(B * Tq, C))
-        d_out_b = _bgrad(ctx, 5, P_out_b, dbr)
+        d_out_w = _wgrad(ctx, 4, P_out_w, dbr, o.view(B * Tq, C), defer=DEFER_BRIDGE)
+        d_out_b = _bgrad(ctx, 5, P_out_b, dbr, defer=DEFER_BRIDGE)
         do = K.linear_dx(dbr, out_w).view(B, Tq, C)
         # packed in_proj gradients: written into the sinks (accumulate) or fresh buffers
         sw = _sink(P_in_w, ctx) if _need(ctx, 2) else None

@@ -282,6 +282,59 @@ def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
     return ok
 
 
+def gemm_grouped(items, dbias=None):
+    """Weight gradients of different shapes as ONE launch (gvl_gemm_grouped): items =
+    [(dy, x, out)], out += dy^T @ x (dy [K_i, M_i], x [K_i, N_i], out [M_i, N_i], bf16,
+    MN-contiguous operands); dbias: None or a list with a bf16 [M_i] bias grad or None per
+    item, += column sums of dy_i.  Returns False when nothing was launched (the caller runs
+    the problems another way)."""
+    n = len(items)
+    if n == 0:
+        return True
+    arr = (GemmDesc * n)()
+    for i, (a, b, out) in enumerate(items):
+        _dev(a, b)
+        _rowmajor(a, "A")
+        _rowmajor(b, "B")
+        _rowmajor(out, "C")
+        if a.dtype != BF16 or b.dtype != BF16 or out.dtype != BF16:
+            raise TypeError("gvl.gemm_grouped: operands must be bf16")
+        if a.shape[0] != b.shape[0] or tuple(out.shape) != (a.shape[1], b.shape[1]):
+            raise ValueError("gvl.gemm_grouped: shape mismatch")
+        d = arr[i]
+        d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+        d.m, d.n, d.k = a.shape[1], b.shape[1], a.shape[0]
+        d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), out.stride(0)
+        d.a_mn, d.b_mn = 1, 1
+        d.alpha = 1.0
+        d.residual, d.ldr = out.data_ptr(), out.stride(0)
+    da = None
+    if dbias is not None:
+        for t in dbias:
+            if t is not None and (t.dtype != BF16 or not t.is_contiguous()):
+                raise ValueError("gvl.gemm_grouped: dbias must be contiguous bf16")
+        da = (C.c_void_p * n)(*[(t.data_ptr() if t is not None else None) for t in dbias])
+    ev = None
+    if _timer is not None and _timer.dispatch:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        ev[1].record()
+        _L().gvl_set_launch_events(C.c_void_p(ev[0].cuda_event), C.c_void_p(ev[1].cuda_event))
+    try:
+        rc = _L().gvl_gemm_grouped(arr, da, n, _stream())
+        if rc not in (0, -1):
+            _lib.check(rc, "gvl_gemm_grouped")
+    finally:
+        if ev is not None:
+            _L().gvl_set_launch_events(None, None)
+    if rc == 0 and ev is not None:
+        buf = C.create_string_buffer(128)
+        _L().gvl_gemm_batched_kernel_name(buf, 128)
+        flops = sum(2.0 * arr[i].m * arr[i].n * arr[i].k for i in range(n))
+        _timer.records.append((buf.value.decode(), ev[0], ev[1], flops))
+    return rc == 0
+
+
 # ------------------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x2, w, b, eps=1e-5, out=None, stats=True):
     _dev(x2)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 8
+#define GVL_ABI_VERSION 9
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -104,6 +104,14 @@ int gvl_gemm_batched(const gvl_gemm_desc* d, int32_t count, gvl_stream_t stream)
  * non-zero return is a launch failure after the GEMM may have added into C (fatal). */
 int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
                            gvl_stream_t stream);
+/* ABI v9: weight gradients of DIFFERENT shapes in one launch — the Q-Former bridge's deferred
+ * nn.Linear weight grads of one backward (source/gpt2_q_former/model.py:114-168, the
+ * out_proj / MLP Linears' grads that loss.backward() produces, each too few output tiles to
+ * fill the chip alone): each problem a_mn = b_mn = 1, residual == c (C += dY^T X), the same
+ * alpha; dbias[i] (bf16 [m], may be null; the array may be null) += column sums of dY_i.
+ * Returns 0 when launched, -1 when the problems do not qualify and nothing was launched. */
+int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
+                     gvl_stream_t stream);
 /* Process-wide GEMM implementation knob (benchmarking / A-B tests; env GVL_GEMM_IMPL):
  * impl 3 (default) = persistent ping-pong 256x256 kernel (split-K for few tiles) where
  * the work items fill the chip, else the 128x128 LDS-DMA ring; 2 = ring / non-persistent

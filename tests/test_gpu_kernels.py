@@ -809,6 +809,35 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
                 assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
 
 
+def test_gemm_grouped_wgrad(cuda):
+    """gvl_gemm_grouped: weight gradients of different shapes (the Q-Former bridge's deferred
+    out_proj / MLP / projection dW at K = 4096 / 4224 tokens, plus a ragged 200 x 136 one over
+    3 K-steps) in one launch of the AGPR four-wave kernel, out += dy^T x, with the bias sums
+    fused for some problems and not others; each vs its own fp32 reference."""
+    import ctypes as C
+    from gvl import _lib
+    K_ = _k()
+    shapes = [(4096, 768, 768), (4096, 768, 768), (4096, 3072, 768), (4096, 768, 3072),
+              (4224, 768, 1024), (96, 200, 136)]
+    torch.manual_seed(11)
+    dys = [(torch.randn(k, m) * 0.1).to(BF) for k, m, n in shapes]
+    xs = [(torch.randn(k, n) * 0.1).to(BF) for k, m, n in shapes]
+    c0 = [torch.randn(m, n).to(BF) for k, m, n in shapes]
+    b0 = [torch.randn(m).to(BF) for k, m, n in shapes]
+    outs = [c.to(cuda) for c in c0]
+    dbs = [(b.to(cuda) if i % 2 == 0 else None) for i, b in enumerate(b0)]
+    assert K_.gemm_grouped([(dy.to(cuda), x.to(cuda), o) for dy, x, o in zip(dys, xs, outs)], dbias=dbs)
+    buf = C.create_string_buffer(128)
+    _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
+    assert buf.value.decode() == "gemm_w4x_kernel<256, 256, true, true, 6, true>", buf.value
+    torch.cuda.synchronize()
+    for dy, x, c, o, b, db in zip(dys, xs, c0, outs, b0, dbs):
+        ref = dy.float().t() @ x.float() + c.float()
+        assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
+        if db is not None:
+            assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
+
+
 @pytest.mark.parametrize("count,rows,cols", [(12, 16384, 2304), (12, 4096, 768), (3, 1000, 3080),
                                              (1, 37, 8)])
 @pytest.mark.parametrize("acc", [False, True])

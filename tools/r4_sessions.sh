@@ -239,5 +239,16 @@ r4v)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 ker
     python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
   for w in qf lm; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -25 $O/${w}_table.txt; done
   ;;
+r4x)  # bridge weight gradients deferred and flushed as ONE grouped AGPR launch (gvl_gemm_grouped):
+      # grouped kernel test, GPU suite + smoke, then the Q-Former step A/B (GVL_DEFER_BRIDGE)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "grouped or batched_wgrad" --timeout 200 \
+    --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  suite
+  for x in 1 0 1 0; do
+    GVL_DEFER_BRIDGE=$x timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf_b$x.json 2> $O/qf_b$x.err
+    fatal $? bench_qf
+    echo "qformer defer_bridge=$x $(python -c "import json;d=json.load(open('$O/qf_b$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:44],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
