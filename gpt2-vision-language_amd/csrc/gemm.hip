@@ -525,7 +525,8 @@ extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int3
     p.ldab[i] = d[i].lda, p.ldbb[i] = d[i].ldb, p.ldcb[i] = d[i].ldc;
   }
   if (!gvl::gemm_w4x_grouped_try(p, gvl::as_stream(stream))) return -1;
-  snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, 256, true, true, %d, true>", EPI_RES);
+  snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, %d, true, true, %d, true>", p.bn,
+           EPI_RES);
   GVL_LAUNCH_CHECK("gvl_gemm_grouped");
   return 0;
 }

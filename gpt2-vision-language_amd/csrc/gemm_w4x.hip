@@ -483,6 +483,7 @@ bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s) { return gemm_w4x_dw_tr
 // deferred dW of one backward, 2-16 problems of 768 x 768 .. 3072 x 768 at K = 4096 tokens,
 // bias sums fused): whole-K 256 x 256 tiles, the problems' tile lists concatenated (GemmP::gtile);
 // each problem alone would be 9-36 tiles and a split-K launch + reduce + a column-sum pair.
+// Tiles of 256 x 256 or 256 x 192, whichever fills the last round better.
 // p: batch, Ab / Bb / Cb / Db and the per-problem sizes set by the caller.  GVL_W4X_GR=0 off.
 bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s) {
   static const bool on = [] {
@@ -490,20 +491,29 @@ bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s) {
     return !(e && e[0] == '0');
   }();
   if (!on || w4x_mode() == 0 || p.batch < 1 || p.batch > GVL_MAX_BATCH) return false;
-  int t = 0;
+  int64_t t192 = 0, t256 = 0;
   for (int i = 0; i < p.batch; ++i) {
     if (p.Kb[i] % KS != 0 || p.Kb[i] < 2 * KS || p.Mb[i] % 8 != 0 || p.Nb[i] % 8 != 0 ||
         p.ldab[i] % 8 != 0 || p.ldbb[i] % 8 != 0 || p.ldcb[i] % 8 != 0)
       return false;
+    t192 += ((p.Mb[i] + 255) / 256) * ((p.Nb[i] + 191) / 192);
+    t256 += ((p.Mb[i] + 255) / 256) * ((p.Nb[i] + 255) / 256);
+  }
+  // tile width by last-round fill as for the batched weight gradients (w4x_dw_plan)
+  const int64_t cus = num_cus();
+  auto fill = [&](int64_t tiles) { return (double)tiles / (double)(((tiles + cus - 1) / cus) * cus); };
+  p.bn = fill(t256) >= 0.95 * fill(t192) ? 256 : 192;
+  int t = 0;
+  for (int i = 0; i < p.batch; ++i) {
     p.gtile[i] = t;
-    t += (int)(((p.Mb[i] + 255) / 256) * ((p.Nb[i] + 255) / 256));
+    t += (int)(((p.Mb[i] + 255) / 256) * ((p.Nb[i] + p.bn - 1) / p.bn));
   }
   p.gtile[p.batch] = t;
   p.grouped = 1;
   p.bm = 256;
-  p.bn = 256;
   p.splits = 1;
-  launch_w4x<256, 256, true, true, EPI_RES, true>(p, s);
+  if (p.bn == 256) launch_w4x<256, 256, true, true, EPI_RES, true>(p, s);
+  else launch_w4x<256, 192, true, true, EPI_RES, true>(p, s);
   return true;
 }
 

@@ -126,6 +126,7 @@ _READY_HOOKS = []
 # batches of 2 problems underfill the chip).  GVL_DEFER_WGRAD=0 launches each one in place.
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
 DEFER_BRIDGE = os.environ.get("GVL_DEFER_BRIDGE", "1") != "0"
+DEFER_INPROJ = os.environ.get("GVL_DEFER_INPROJ", "1") != "0"  # MHAFn's packed in_proj slices too
 GROUPED_WGRAD = os.environ.get("GVL_GROUPED_WGRAD", "1") != "0"
 # Queue entries are tagged with the autograd graph task that produced them, and every task
 # that defers queues its OWN end-of-backward flush, which runs only that task's entries: two
@@ -185,6 +186,17 @@ def flush_wgrads(task=None):
     pend = [e[1:] for e in _take(_PENDING, task)]
     pend_b = [e[1:] for e in _take(_PENDING_B, task)]
     _BLOCKS_SEEN.pop(task, None)
+    # a parameter may have several queued entries (the packed in_proj's row slices): its
+    # grad-ready hook runs once, after the last of them is launched
+    left = {}
+    for e in pend + pend_b:
+        left[id(e[0])] = left.get(id(e[0]), 0) + 1
+
+    def _done(p):
+        left[id(p)] -= 1
+        if left[id(p)] == 0:
+            _ready(p)
+
     # a bias gradient over the same dY as a queued weight gradient rides in that batched GEMM
     # (gvl_gemm_batched_dbias: row sums of dY^T from the same operand tiles); each bias pairs
     # with ONE weight gradient (popped when used), so a dY shared by two weight gradients
@@ -207,7 +219,7 @@ def flush_wgrads(task=None):
                dy2.device, st)
         groups.setdefault(key, []).append((p, g, dy2, x2))
     if GROUPED_WGRAD and len(groups) >= 2:
-        groups = _flush_grouped(groups, paired)
+        groups = _flush_grouped(groups, paired, _done)
     order = list(groups.items())
     ready = []
     for key, items in order:
@@ -228,7 +240,7 @@ def flush_wgrads(task=None):
                 if fused:
                     ready += [b[0] for b in bias]
         for p in ready:
-            _ready(p)
+            _done(p)
         ready = []
     for k, (p, g) in paired.items():  # (unreachable unless a weight entry vanished)
         raise RuntimeError(f"gvl: unpaired deferred bias gradient {k}")
@@ -243,10 +255,10 @@ def flush_wgrads(task=None):
                     K.colsum_batched([d for _, _, d in chunk], [g for _, g, _ in chunk],
                                      accumulate=True)
                     for p, *_ in chunk:
-                        _ready(p)
+                        _done(p)
 
 
-def _flush_grouped(groups, paired):
+def _flush_grouped(groups, paired, done):
     """Every queued weight gradient of the flush as one grouped launch when they share a stream,
     number at most 16 and run over at most 8192 tokens (the bridge's; the LM blocks' K = 16384
     batches stay per shape); returns the groups left to the per-shape path."""
@@ -263,9 +275,9 @@ def _flush_grouped(groups, paired):
                 paired[_dkey(d)] = b
         return groups
     for (p, _, _, _), b in zip(items, bias):
-        _ready(p)
+        done(p)
         if b is not None:
-            _ready(b[0])
+            done(b[0])
     return {}
 
 
@@ -699,12 +711,21 @@ class MHAFn(torch.autograd.Function):
         tw = sw if sw is not None else din_w
         tb = sb if sb is not None else din_b
 
+        # into the arena sinks the row slices are deferred like the other bridge gradients
+        # (one grouped launch at the end of backward; the grad-ready hook after the last slice)
+        dfw = sw is not None and DEFER_BRIDGE and DEFER_INPROJ and DEFER_WGRAD
+        dfb = sb is not None and DEFER_BRIDGE and DEFER_INPROJ and DEFER_WGRAD
+
         def wg(dy_, x_, rows):
-            if tw is not None:
+            if dfw:
+                _defer_wgrad(P_in_w, tw[rows], dy_, x_)
+            elif tw is not None:
                 K.linear_dw(dy_, x_, out=tw[rows], residual=tw[rows] if sw is not None else None)
 
         def bg(dy_, rows):
-            if tb is not None:
+            if dfb:  # (dqkv / dqp / dkvp: fresh contiguous buffers)
+                _defer_wgrad(P_in_b, tb[rows], dy_, None)
+            elif tb is not None:
                 K.colsum(dy_, out=tb[rows], accumulate=sb is not None)
 
         dq_in = dkv_in = None
@@ -736,9 +757,9 @@ class MHAFn(torch.autograd.Function):
                 dq_in = K.linear_dx(dqp, in_w[:C]).view(B, Tq, C)
             if _need(ctx, 1):
                 dkv_in = K.linear_dx(dkvp, in_w[C:]).view(B, Tk, C)
-        if sw is not None:
+        if sw is not None and not dfw:
             _ready(P_in_w)
-        if sb is not None:
+        if sb is not None and not dfb:
             _ready(P_in_b)
         return dq_in, dkv_in, din_w, din_b, d_out_w, d_out_b, dres, None, None, None, None, None
 

@@ -809,7 +809,13 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
                 assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
 
 
-def test_gemm_grouped_wgrad(cuda):
+@pytest.mark.parametrize("shapes", [
+    [(4096, 768, 768), (4096, 768, 768), (4096, 3072, 768), (4096, 768, 3072), (4224, 768, 1024),
+     (96, 200, 136)],
+    # the Q-Former step's whole flush incl. the in_proj row slices: 256 x 192 tiles fill better
+    [(4096, 768, 768)] * 4 + [(4096, 3072, 768)] * 2 + [(4096, 768, 3072)] * 2 + [(4224, 768, 1024)]
+    + [(4096, 2304, 768)] * 2 + [(4096, 768, 768)] * 2 + [(4224, 1536, 768)] * 2])
+def test_gemm_grouped_wgrad(cuda, shapes):
     """gvl_gemm_grouped: weight gradients of different shapes (the Q-Former bridge's deferred
     out_proj / MLP / projection dW at K = 4096 / 4224 tokens, plus a ragged 200 x 136 one over
     3 K-steps) in one launch of the AGPR four-wave kernel, out += dy^T x, with the bias sums
@@ -817,9 +823,7 @@ def test_gemm_grouped_wgrad(cuda):
     import ctypes as C
     from gvl import _lib
     K_ = _k()
-    shapes = [(4096, 768, 768), (4096, 768, 768), (4096, 3072, 768), (4096, 768, 3072),
-              (4224, 768, 1024), (96, 200, 136)]
-    torch.manual_seed(11)
+    torch.manual_seed(len(shapes))
     dys = [(torch.randn(k, m) * 0.1).to(BF) for k, m, n in shapes]
     xs = [(torch.randn(k, n) * 0.1).to(BF) for k, m, n in shapes]
     c0 = [torch.randn(m, n).to(BF) for k, m, n in shapes]
@@ -829,7 +833,8 @@ def test_gemm_grouped_wgrad(cuda):
     assert K_.gemm_grouped([(dy.to(cuda), x.to(cuda), o) for dy, x, o in zip(dys, xs, outs)], dbias=dbs)
     buf = C.create_string_buffer(128)
     _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
-    assert buf.value.decode() == "gemm_w4x_kernel<256, 256, true, true, 6, true>", buf.value
+    assert buf.value.decode() in ("gemm_w4x_kernel<256, 256, true, true, 6, true>",
+                                  "gemm_w4x_kernel<256, 192, true, true, 6, true>"), buf.value
     torch.cuda.synchronize()
     for dy, x, c, o, b, db in zip(dys, xs, c0, outs, b0, dbs):
         ref = dy.float().t() @ x.float() + c.float()

@@ -250,5 +250,16 @@ r4x)  # bridge weight gradients deferred and flushed as ONE grouped AGPR launch 
     echo "qformer defer_bridge=$x $(python -c "import json;d=json.load(open('$O/qf_b$x.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:44],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
   done
   ;;
+r4y)  # the MHA in_proj row slices deferred into the grouped launch too (GVL_DEFER_INPROJ): grouped tests,
+      # GPU suite + smoke, Q-Former step A/B (in_proj deferred / bridge deferred without in_proj / nothing)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "grouped" --timeout 200 \
+    --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  suite
+  for v in "1 1" "1 0" "0 0" "1 1" "1 0" "0 0"; do set -- $v
+    GVL_DEFER_BRIDGE=$1 GVL_DEFER_INPROJ=$2 timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf_$1$2.json 2> $O/qf_$1$2.err
+    fatal $? bench_qf
+    echo "qformer bridge=$1 inproj=$2 $(python -c "import json;d=json.load(open('$O/qf_$1$2.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
