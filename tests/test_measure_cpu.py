@@ -57,5 +57,5 @@ def test_committed_traffic_covers_bench_dominant_kernels():
         t = json.load(f)["workloads"]
     # the dominant GEMMs of the round-4 bench lines (profiles/r4/bench_r4v.json), with MFMA busy
     # and the exact MFMA-rate fraction
-    for wl, name in (("lm", "gemm_w4x_kernel<256, 256, true, true, 6>"), ("qf", "gemm_w4d_kernel<false, 2>")):
+    for wl, name in (("lm", "gemm_w4x_kernel<256, 256, true, true, 6, false>"), ("qf", "gemm_w4d_kernel<false, 2>")):
         assert t[wl][name]["hbm_bytes"] > 0 and 0 < t[wl][name]["mfma_rate_frac"] < 1

@@ -261,5 +261,10 @@ r4y)  # the MHA in_proj row slices deferred into the grouped launch too (GVL_DEF
     echo "qformer bridge=$1 inproj=$2 $(python -c "import json;d=json.load(open('$O/qf_$1$2.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done
   ;;
+r4z)  # rocprofv3 kernel stats of the Q-Former step at this head
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 45 > $O/qf_table.txt; cat $O/qf_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
