@@ -500,12 +500,13 @@ extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int3
                                 gvl_stream_t stream) {
   g_batched_name[0] = 0;
   GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_grouped: bad arguments");
-  if (count > GVL_MAX_BATCH || env().impl < 3 || env().cfg >= 0) return -1;
+  if (count > GVL_MAX_GROUP || env().impl < 3 || env().cfg >= 0) return -1;
   for (int i = 0; i < count; ++i) {
     const gvl_gemm_desc& e = d[i];
     if (!(e.a_mn && e.b_mn && e.residual == e.c && e.ldr == e.ldc && e.alpha == d[0].alpha &&
           !e.alpha_ptr && !e.bias && !e.act && !e.dact && !e.gate && e.drop_p == 0.f && !e.c_fp32 &&
-          e.m > 0 && e.n > 0 && e.k > 0 && gvl::aligned16(e.a) && gvl::aligned16(e.b) &&
+          e.m > 0 && e.n > 0 && e.k > 0 && e.m < (1 << 30) && e.n < (1 << 30) && e.k < (1 << 30) &&
+          e.lda < (1 << 30) && e.ldb < (1 << 30) && e.ldc < (1 << 30) && gvl::aligned16(e.a) && gvl::aligned16(e.b) &&
           gvl::aligned16(e.c)))
       return -1;
   }
@@ -516,13 +517,13 @@ extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int3
   p.tickets = nullptr;
   p.nticket = 0;
   p.batch = count;
-  for (int i = 0; i < GVL_MAX_BATCH; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
+  for (int i = 0; i < GVL_MAX_GROUP; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
   for (int i = 0; i < count; ++i) {
     p.Ab[i] = static_cast<const bf16_t*>(d[i].a);
     p.Bb[i] = static_cast<const bf16_t*>(d[i].b);
     p.Cb[i] = d[i].c;
-    p.Mb[i] = d[i].m, p.Nb[i] = d[i].n, p.Kb[i] = d[i].k;
-    p.ldab[i] = d[i].lda, p.ldbb[i] = d[i].ldb, p.ldcb[i] = d[i].ldc;
+    p.Mb[i] = (int32_t)d[i].m, p.Nb[i] = (int32_t)d[i].n, p.Kb[i] = (int32_t)d[i].k;
+    p.ldab[i] = (int32_t)d[i].lda, p.ldbb[i] = (int32_t)d[i].ldb, p.ldcb[i] = (int32_t)d[i].ldc;
   }
   if (!gvl::gemm_w4x_grouped_try(p, gvl::as_stream(stream))) return -1;
   snprintf(g_batched_name, sizeof g_batched_name, "gemm_w4x_kernel<256, %d, true, true, %d, true>", p.bn,

@@ -4,6 +4,8 @@
 #include "../../include/gvl.h"
 
 #define GVL_MAX_BATCH 16
+// problems of one grouped launch: every LM weight gradient of a backward flush (12 blocks x 4)
+#define GVL_MAX_GROUP 48
 
 struct GemmP {
   const bf16_t* A;
@@ -43,19 +45,20 @@ struct GemmP {
   // batched launch (gvl_gemm_batched, gemm_pp3_kernel): `batch` problems of one shape, work
   // items batch-major, per-problem operands below (batch == 1: A, B, C, residual above)
   int batch;
-  const bf16_t* Ab[GVL_MAX_BATCH];
-  const bf16_t* Bb[GVL_MAX_BATCH];
-  void* Cb[GVL_MAX_BATCH];
+  const bf16_t* Ab[GVL_MAX_GROUP];
+  const bf16_t* Bb[GVL_MAX_GROUP];
+  void* Cb[GVL_MAX_GROUP];
   // optional per-problem bf16 [M] bias gradients, Db[i] += row sums of op(A_i) over K (the
   // nn.Linear bias grad next to its weight grad dW = dY^T X: A = dY^T), computed by the
   // weight-gradient tiles of the first column block with MFMAs against a ones fragment
-  void* Db[GVL_MAX_BATCH];
+  void* Db[GVL_MAX_GROUP];
   // grouped launch (gvl_gemm_grouped, gemm_w4x_kernel GR): problems of different sizes, the
-  // per-problem sizes / strides here, gtile[i] = problem i's first work item (gtile[batch] = all)
+  // per-problem sizes / strides here (32-bit: the kernel argument block stays ~3.2 KB with 48
+  // problems), gtile[i] = problem i's first work item (gtile[batch] = all)
   int grouped;
-  int64_t Mb[GVL_MAX_BATCH], Nb[GVL_MAX_BATCH], Kb[GVL_MAX_BATCH];
-  int64_t ldab[GVL_MAX_BATCH], ldbb[GVL_MAX_BATCH], ldcb[GVL_MAX_BATCH];
-  int gtile[GVL_MAX_BATCH + 1];
+  int32_t Mb[GVL_MAX_GROUP], Nb[GVL_MAX_GROUP], Kb[GVL_MAX_GROUP];
+  int32_t ldab[GVL_MAX_GROUP], ldbb[GVL_MAX_GROUP], ldcb[GVL_MAX_GROUP];
+  int gtile[GVL_MAX_GROUP + 1];
 };
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each

@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   short8_t ones;
 #pragma unroll
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
+  const uint32_t db_hi = (wave & 1) ? 0xFFFFFFFFu : 0u;  // odd waves sum fragments 4..7
   // alpha x *alpha_ptr read once, before any DMA is in flight
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     // then 48 MFMAs with step c+1's 14 fragment reads (buffer NXT) and step c+NS-1's 7 DMA
     // pieces issued between them.  FULL: a step with both (every step but the last NS - 1), no
     // branches; otherwise each is conditional.
-#define W4X_STEP(c, CUR, NXT, FULL)                                                            \
+#define W4X_STEP(c, CUR, NXT, FULL, DBS)                                                       \
   do {                                                                                         \
     w4x_wait(fa[CUR], fb[CUR]);                                                                \
     if (FULL) {                                                                                \
@@ -313,12 +314,15 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     }                                                                                          \
     /* builtin MFMAs: hipcc may copy bacc at the branch joins, and must see the MFMA to */    \
     /* put the wait states in front of such a copy */                                          \
-    if (DB && do_db) {                                                                         \
-      if ((wave & 1) == 0) {                                                                   \
-        _Pragma("unroll") for (int k = 0; k < 4; ++k) bacc[k] = mfma16(ones, fa[CUR][k], bacc[k]); \
-      } else {                                                                                 \
-        _Pragma("unroll") for (int k = 0; k < 4; ++k)                                          \
-          bacc[k] = mfma16(ones, fa[CUR][4 + k], bacc[k]);                                     \
+    /* bias sums: the wave's row half picked by bit masks (a branch on the parity made hipcc */ \
+    /* copy the sums at its join after waiting for the MFMAs; a ?: on the fragments went */      \
+    /* through scratch) */                                                                     \
+    if (DBS && do_db) {                                                                        \
+      _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                          \
+        const u32x4_t lo_ = __builtin_bit_cast(u32x4_t, fa[CUR][k]);                           \
+        const u32x4_t hi_ = __builtin_bit_cast(u32x4_t, fa[CUR][4 + k]);                       \
+        const short8_t x_ = __builtin_bit_cast(short8_t, (hi_ & db_hi) | (lo_ & ~db_hi));       \
+        bacc[k] = mfma16(ones, x_, bacc[k]);                                                   \
       }                                                                                        \
     }                                                                                          \
   } while (0)
@@ -326,12 +330,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
     const int nfull = nks - (NS - 1);  // steps c < nfull issue both their reads and a DMA
     int c = 0;
     for (; c + 1 < nfull; c += 2) {
-      W4X_STEP(c, 0, 1, true);
-      W4X_STEP(c + 1, 1, 0, true);
+      W4X_STEP(c, 0, 1, true, DB);
+      W4X_STEP(c + 1, 1, 0, true, DB);
     }
     for (; c < nks; c += 2) {  // c even: fragments in buffer 0
-      W4X_STEP(c, 0, 1, false);
-      if (c + 1 < nks) W4X_STEP(c + 1, 1, 0, false);
+      W4X_STEP(c, 0, 1, false, DB);
+      if (c + 1 < nks) W4X_STEP(c + 1, 1, 0, false, DB);
     }
 #undef W4X_STEP
 #undef W4X_PIECE_A
@@ -490,7 +494,7 @@ bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s) {
     const char* e = getenv("GVL_W4X_GR");
     return !(e && e[0] == '0');
   }();
-  if (!on || w4x_mode() == 0 || p.batch < 1 || p.batch > GVL_MAX_BATCH) return false;
+  if (!on || w4x_mode() == 0 || p.batch < 1 || p.batch > GVL_MAX_GROUP) return false;
   int64_t t192 = 0, t256 = 0;
   for (int i = 0; i < p.batch; ++i) {
     if (p.Kb[i] % KS != 0 || p.Kb[i] < 2 * KS || p.Mb[i] % 8 != 0 || p.Nb[i] % 8 != 0 ||

@@ -127,7 +127,13 @@ _READY_HOOKS = []
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
 DEFER_BRIDGE = os.environ.get("GVL_DEFER_BRIDGE", "1") != "0"
 DEFER_INPROJ = os.environ.get("GVL_DEFER_INPROJ", "1") != "0"  # MHAFn's packed in_proj slices too
-GROUPED_WGRAD = os.environ.get("GVL_GROUPED_WGRAD", "1") != "0"
+# Grouped flush (gvl_gemm_grouped) of the queued weight gradients of one stream over <= 8192
+# tokens: 2 (default) up to 48 problems (the cross-att decoder's 12 blocks' flush: +1.9 % on its
+# step, profiles/r4/grouped48_r4g48.txt), 1 up to 16 (the Q-Former bridge's), 0 off.  The LM's
+# K = 16384 flushes stay per-shape batches: all 48 of them as one grouped launch measured 3070
+# vs 2942 us and the LM step 924k vs 933.6k tokens/s (same box).
+GROUPED_WGRAD = int(os.environ.get("GVL_GROUPED_WGRAD", "2"))
+GROUPED_MAX = 48
 # Queue entries are tagged with the autograd graph task that produced them, and every task
 # that defers queues its OWN end-of-backward flush, which runs only that task's entries: two
 # backward passes (two models, two threads, a nested reentrant backward) never consume each
@@ -260,10 +266,12 @@ def flush_wgrads(task=None):
 
 def _flush_grouped(groups, paired, done):
     """Every queued weight gradient of the flush as one grouped launch when they share a stream,
-    number at most 16 and run over at most 8192 tokens (the bridge's; the LM blocks' K = 16384
-    batches stay per shape); returns the groups left to the per-shape path."""
+    run over at most 8192 tokens and number at most GROUPED_MAX (GROUPED_WGRAD 1: 16); returns
+    the groups left to the per-shape path."""
     items = [it for its in groups.values() for it in its]
-    if len({key[-1] for key in groups}) != 1 or len(items) > 16 or any(it[2].shape[0] > 8192 for it in items):
+    if len({key[-1] for key in groups}) != 1 or any(it[2].shape[0] > 8192 for it in items):
+        return groups
+    if len(items) > (GROUPED_MAX if GROUPED_WGRAD >= 2 else 16):
         return groups
     bias = [paired.pop(_dkey(d), None) for _, _, d, _ in items]
     with torch.cuda.stream(next(iter(groups))[-1]):

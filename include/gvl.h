@@ -109,6 +109,8 @@ int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t c
  * out_proj / MLP Linears' grads that loss.backward() produces, each too few output tiles to
  * fill the chip alone): each problem a_mn = b_mn = 1, residual == c (C += dY^T X), the same
  * alpha; dbias[i] (bf16 [m], may be null; the array may be null) += column sums of dY_i.
+ * count <= 48 (round 4: also every GPT-2 block's four weight grads of one LM backward flush,
+ * train_gpt2.py:55-59,71-74, sizes and strides < 2^30).
  * Returns 0 when launched, -1 when the problems do not qualify and nothing was launched. */
 int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
                      gvl_stream_t stream);

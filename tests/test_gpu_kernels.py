@@ -814,7 +814,10 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
      (96, 200, 136)],
     # the Q-Former step's whole flush incl. the in_proj row slices: 256 x 192 tiles fill better
     [(4096, 768, 768)] * 4 + [(4096, 3072, 768)] * 2 + [(4096, 768, 3072)] * 2 + [(4224, 768, 1024)]
-    + [(4096, 2304, 768)] * 2 + [(4096, 768, 768)] * 2 + [(4224, 1536, 768)] * 2])
+    + [(4096, 2304, 768)] * 2 + [(4096, 768, 768)] * 2 + [(4224, 1536, 768)] * 2,
+    # an LM backward flush (12 blocks x c_attn / attn.c_proj / c_fc / mlp.c_proj, 48 problems,
+    # the GVL_MAX_GROUP limit) at 1024 of its 16384 tokens
+    [(1024, 768, 3072), (1024, 3072, 768), (1024, 768, 768), (1024, 2304, 768)] * 12])
 def test_gemm_grouped_wgrad(cuda, shapes):
     """gvl_gemm_grouped: weight gradients of different shapes (the Q-Former bridge's deferred
     out_proj / MLP / projection dW at K = 4096 / 4224 tokens, plus a ragged 200 x 136 one over
@@ -841,6 +844,20 @@ def test_gemm_grouped_wgrad(cuda, shapes):
         assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3
         if db is not None:
             assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
+
+
+def test_gemm_grouped_declines_past_limit(cuda):
+    """gvl_gemm_grouped returns -1 (gemm_grouped False) for 49 problems, launching nothing."""
+    K_ = _k()
+    dy = torch.randn(64, 64, device=cuda).to(BF)
+    x = torch.randn(64, 64, device=cuda).to(BF)
+    outs = [torch.zeros(64, 64, device=cuda, dtype=BF) for _ in range(49)]
+    assert not K_.gemm_grouped([(dy, x, o) for o in outs])
+    assert K_.gemm_grouped([(dy, x, o) for o in outs[:48]])
+    torch.cuda.synchronize()
+    assert float(outs[48].float().abs().max()) == 0.0
+    ref = dy.float().t() @ x.float()
+    assert rel_err(outs[47].float().cpu().numpy(), ref.cpu().numpy()) < 8e-3
 
 
 @pytest.mark.parametrize("count,rows,cols", [(12, 16384, 2304), (12, 4096, 768), (3, 1000, 3080),

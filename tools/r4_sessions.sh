@@ -266,5 +266,35 @@ r4z)  # rocprofv3 kernel stats of the Q-Former step at this head
     python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
   f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 45 > $O/qf_table.txt; cat $O/qf_table.txt
   ;;
+r4db)  # fused bias sums of the batched AGPR dW without per-step branch joins: kernel tests, wgrad
+       # (gvl vs gvl + dbias per shape), LM step twice
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "test_gemm_w4x or batched_wgrad or grouped" \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad.log 2>&1; fatal $? wgrad; grep x12 $O/wgrad.log | cut -c1-220
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_$r.json 2> $O/lm_$r.err
+    fatal $? bench_lm
+    echo "lm $(python -c "import json;d=json.load(open('$O/lm_$r.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:48],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:6]])")"
+  done
+  timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/qf.json 2> $O/qf.err; fatal $? bench_qf
+  echo "qformer $(python -c "import json;d=json.load(open('$O/qf.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  ;;
+r4g48)  # every LM weight gradient of a flush as ONE grouped launch (GVL_GROUPED_WGRAD=2, 48 problems):
+        # grouped kernel tests, wgrad (grouped vs the four batches), LM / caption step A/B, GPU suite
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "grouped or batched_wgrad or test_gemm_w4x" \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > $O/kt.log 2>&1; rc=$?; tail -3 $O/kt.log; fatal $rc kernel_tests
+  timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad.log 2>&1; fatal $? wgrad; cut -c1-200 $O/wgrad.log
+  for g in 2 1 2 1; do
+    GVL_GROUPED_WGRAD=$g timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline > $O/lm_g$g.json 2> $O/lm_g$g.err
+    fatal $? bench_lm
+    echo "lm grouped=$g $(python -c "import json;d=json.load(open('$O/lm_g$g.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:48],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:4]])")"
+  done
+  for w in qformer cross; do for g in 2 1; do
+    GVL_GROUPED_WGRAD=$g timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > $O/${w}_g$g.json 2> $O/${w}_g$g.err
+    fatal $? bench_$w
+    echo "$w grouped=$g $(python -c "import json;d=json.load(open('$O/${w}_g$g.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
+  suite
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac

@@ -2,7 +2,8 @@
 the 12 blocks' dW += dY^T X of one shape, fused bias column sums) against the hipBLASLt
 yardstick (torch.bmm over the same transposed views, no accumulate, no bias), HIP events,
 median of 5 x 10 launches.  python tools/wgrad_diag.py [K]  (K = tokens per micro-step,
-default 16384 = B 16 x T 1024)."""
+default 16384 = B 16 x T 1024).  Last line: all 48 problems as ONE grouped launch
+(gvl_gemm_grouped, the default LM flush since round 4) against the sum of the four batches."""
 import os
 import ctypes as C
 import statistics
@@ -36,6 +37,7 @@ def timeit(fn, reps=10, rounds=5):
 
 
 torch.manual_seed(0)
+ALL, tot_b, tot_fl = [], 0.0, 0.0
 for name, M, N in SHAPES:
     dy = [(torch.rand(KT, M, device=dev) - 0.5).to(torch.bfloat16) for _ in range(L)]
     x = [(torch.rand(KT, N, device=dev) - 0.5).to(torch.bfloat16) for _ in range(L)]
@@ -54,5 +56,15 @@ for name, M, N in SHAPES:
     print(f"{name:12s} M={M:5d} N={N:5d} K={KT} x{L}: gvl+dbias {tb:8.1f}us ({fl / tb / 1e6:6.0f} TF/s)  "
           f"gvl {tn:8.1f}us ({fl / tn / 1e6:6.0f} TF/s)  torch.bmm {ty:8.1f}us ({fl / ty / 1e6:6.0f} TF/s)  [{kname}]",
           flush=True)
-    del dy, x, g, db, items, DY, X
+    tot_b += tb
+    tot_fl += fl
+    ALL.append((dy, x, g, db))
+    del items, DY, X
     torch.cuda.empty_cache()
+gitems = [(f[0][i], f[1][i], f[2][i]) for i in range(L) for f in ALL]
+gdb = [f[3][i] for i in range(L) for f in ALL]
+assert K.gemm_grouped(gitems, dbias=gdb)
+_lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
+tg = timeit(lambda: K.gemm_grouped(gitems, dbias=gdb))
+print(f"grouped x{len(gitems)} (+dbias): {tg:8.1f}us ({tot_fl / tg / 1e6:6.0f} TF/s)  vs the four batches "
+      f"{tot_b:8.1f}us ({tot_fl / tot_b / 1e6:6.0f} TF/s)  [{buf.value.decode()}]", flush=True)
