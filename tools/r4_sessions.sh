@@ -229,7 +229,7 @@ r4u)  # persistent AGPR four-wave kernel (gemm_w4p.hip) on the wide short-K shap
     echo "qformer w4p=$x $(python -c "import json;d=json.load(open('$O/qf_p$x.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done
   ;;
-r4v|r4fin)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of both steps
+r4v|r4fin|r4fin2)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of both steps
   suite
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
   python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],d['caption_qformer']['value'])"
