@@ -70,7 +70,7 @@ r4g)  # attention forward: LDS-DMA ring vs register staging (GVL_ATTN_FWD_DMA), 
     fatal $? bench_lm; echo "lm fwd_dma=$f $(python -c "import json;d=json.load(open('$O/lm_f$f.json'));print(d['value'])")"
   done
   ;;
-r4h)  # PMC passes of both bench steps (HBM bytes, MFMA busy, achieved clock per kernel)
+r4h|r4w3)  # PMC passes of both bench steps (HBM bytes, MFMA busy, achieved clock per kernel)
   bash tools/pmc_traffic.sh $S; rc=$?; fatal $rc pmc
   python -c "import json;d=json.load(open('gpurun_out/pmc_traffic_$S.json'));[print(w,k,v) for w in d['workloads'] for k,v in sorted(d['workloads'][w].items(),key=lambda kv:-kv[1].get('launches',0))[:6]]"
   ;;
