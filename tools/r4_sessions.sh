@@ -321,5 +321,17 @@ r4dbs)  # bias sums spread over the column blocks (libgvl_dbs1.so: GVL_W4X_DBSPR
     echo "lm $v $(python -c "import json;d=json.load(open('$O/lm_$v.json'));r=d['roofline'];print(d['value'],d.get('step_mfma_frac'),[(g['kernel'][:48],g['ms_per_step'],g['avg_us']) for g in r['top_gemms'][:3]])")"
   done
   ;;
+r4ln)  # LayerNorm forward with 2 / 4 rows per half-wave in flight (GVL_LN_RPH builds): LN tests on each,
+       # launch times at the bench shapes, alternated
+  for v in ln2 ln4; do
+    GVL_LIB=$LIBDIR/libgvl_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "layernorm" \
+      --timeout 120 --timeout-method thread -p no:cacheprovider > $O/kt_$v.log 2>&1; rc=$?; tail -1 $O/kt_$v.log; fatal $rc ln_tests
+  done
+  for v in base ln2 ln4 base ln2 ln4; do
+    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
+    GVL_LIB=$L timeout -k 10 200 python -u tools/ln_one.py > $O/ln_$v.log 2>&1; fatal $? ln_one
+    echo "== $v"; grep ln_ $O/ln_$v.log
+  done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
