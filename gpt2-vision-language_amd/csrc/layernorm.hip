@@ -13,7 +13,13 @@ namespace {
 
 constexpr int LN_FWD_NT = 256;   // 8 rows per block
 constexpr int LN_BWD_NT = 256;   // 4 waves, one row each (+1 prefetched)
-constexpr int LN_BWD_MAXB = 1024;
+// backward blocks (rows per wave = rows / (4 x blocks)): 512 measured best of 256 / 384 / 512 /
+// 1024 / 2048 (16384 x 768 22.2-22.5 vs 23.1-23.4 us at 1024, 8064 x 768 15.0 vs 16.5, 4224 x 1024
+// 14.3 vs 15.3, incl. the finalize; profiles/r4/ln_bwd_blocks_r4lnb.txt)
+#ifndef GVL_LN_BWD_MAXB
+#define GVL_LN_BWD_MAXB 512
+#endif
+constexpr int LN_BWD_MAXB = GVL_LN_BWD_MAXB;
 
 GVL_DEV float half_sum(float v) {
 #pragma unroll
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(1024) void ln_bwd_finalize(const float* __restrict_
   *dst = f2bf(t);
 }
 
-// >= 2 rows per wave, <= 1024 blocks (4 per CU: 16 waves, ~32 rows in flight per CU).
+// >= 2 rows per wave, <= LN_BWD_MAXB blocks (512: 2 per CU, 8 waves, ~16 rows in flight per CU).
 int ln_bwd_blocks(int64_t rows) {
   int64_t nb = (rows + 7) / 8;
   if (nb > LN_BWD_MAXB) nb = LN_BWD_MAXB;

@@ -43,3 +43,17 @@ for rows, C in [(16384, 768), (8064, 768), (4096, 768), (4224, 1024)]:
     tf = timeit(g.replay, reps=2) / 50
     gb = 2.0 * rows * C * 2 / 1e9
     print(f"ln_fwd rows={rows:6d} C={C:5d}: {tf:7.2f} us  {gb / tf * 1e6 / 1e3:6.2f} TB/s", flush=True)
+    _, mean, rstd = K.layernorm_fwd(x, w, b, out=y)
+    dy = torch.randn(rows, C, device=dev).to(torch.bfloat16)
+    res = torch.randn(rows, C, device=dev).to(torch.bfloat16)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(C, device=dev, dtype=torch.bfloat16)
+    db = torch.zeros(C, device=dev, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()  # the LM's form: dx = residual grad + LN', dw / db accumulated
+    with torch.cuda.graph(g2):
+        for _ in range(50):
+            K.layernorm_bwd(dy, x, w, mean, rstd, dx=dx, dw=dw, db=db, accumulate_wb=True, residual=res)
+    tb = timeit(g2.replay, reps=2) / 50
+    gb = 4.0 * rows * C * 2 / 1e9
+    print(f"ln_bwd rows={rows:6d} C={C:5d}: {tb:7.2f} us  {gb / tb * 1e6 / 1e3:6.2f} TB/s (+ finalize)", flush=True)

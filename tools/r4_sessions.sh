@@ -229,7 +229,7 @@ r4u)  # persistent AGPR four-wave kernel (gemm_w4p.hip) on the wide short-K shap
     echo "qformer w4p=$x $(python -c "import json;d=json.load(open('$O/qf_p$x.json'));print(d['value'],d.get('step_mfma_frac'))")"
   done
   ;;
-r4v|r4fin|r4fin2)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of both steps
+r4v|r4fin|r4fin2|r4fin3)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of both steps
   suite
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
   python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],d['caption_qformer']['value'])"
@@ -331,6 +331,19 @@ r4ln)  # LayerNorm forward with 2 / 4 rows per half-wave in flight (GVL_LN_RPH b
     L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
     GVL_LIB=$L timeout -k 10 200 python -u tools/ln_one.py > $O/ln_$v.log 2>&1; fatal $? ln_one
     echo "== $v"; grep ln_ $O/ln_$v.log
+  done
+  ;;
+r4lnb|r4lnb2)  # LayerNorm backward block count (GVL_LN_BWD_MAXB builds vs 1024): LN tests, launch times
+  V1="lnb512 lnb2048"; V2="base lnb512 lnb2048 base lnb512 lnb2048"
+  [ $S = r4lnb2 ] && V1="lnb256 lnb384" && V2="base lnb512 lnb256 lnb384 base lnb512 lnb256 lnb384"
+  for v in $V1; do
+    GVL_LIB=$LIBDIR/libgvl_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "layernorm" \
+      --timeout 120 --timeout-method thread -p no:cacheprovider > $O/kt_$v.log 2>&1; rc=$?; tail -1 $O/kt_$v.log; fatal $rc ln_tests
+  done
+  for v in $V2; do
+    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
+    GVL_LIB=$L timeout -k 10 200 python -u tools/ln_one.py > $O/ln_$v.log 2>&1; fatal $? ln_one
+    echo "== $v"; grep ln_bwd $O/ln_$v.log
   done
   ;;
 *) echo "unknown session $S"; exit 2;;
