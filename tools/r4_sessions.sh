@@ -296,14 +296,6 @@ r4g48)  # every LM weight gradient of a flush as ONE grouped launch (GVL_GROUPED
   done; done
   suite
   ;;
-r4dbk)  # where the fused bias sums' cost comes from: timing-only builds with 0 / 1 / 2 of the 4
-        # bias MFMAs per step (GVL_W4X_DBK), gvl vs gvl + dbias per family
-  for v in base dbk0 dbk1 dbk2 base; do
-    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
-    GVL_LIB=$L timeout -k 10 300 python -u tools/wgrad_diag.py > $O/wgrad_$v.log 2>&1; fatal $? wgrad
-    echo "== $v"; grep x12 $O/wgrad_$v.log | cut -c1-112
-  done
-  ;;
 r4dbs)  # bias sums spread over the column blocks (libgvl_dbs1.so: GVL_W4X_DBSPREAD) vs the shipped
         # build (all in column block 0): dbias kernel tests on the variant, wgrad per family, LM A/B
   GVL_LIB=$LIBDIR/libgvl_dbs1.so timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -q -x \
