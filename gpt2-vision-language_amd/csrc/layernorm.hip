@@ -15,7 +15,8 @@ constexpr int LN_FWD_NT = 256;   // 8 rows per block
 constexpr int LN_BWD_NT = 256;   // 4 waves, one row each (+1 prefetched)
 // backward blocks (rows per wave = rows / (4 x blocks)): 512 measured best of 256 / 384 / 512 /
 // 1024 / 2048 (16384 x 768 22.2-22.5 vs 23.1-23.4 us at 1024, 8064 x 768 15.0 vs 16.5, 4224 x 1024
-// 14.3 vs 15.3, incl. the finalize; profiles/r4/ln_bwd_blocks_r4lnb.txt)
+// 14.3 vs 15.3, incl. the finalize, back to back; no measurable change inside the steps;
+// profiles/r4/ln_bwd_blocks_r4lnb.txt)
 #ifndef GVL_LN_BWD_MAXB
 #define GVL_LN_BWD_MAXB 512
 #endif

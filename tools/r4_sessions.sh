@@ -338,5 +338,13 @@ r4lnb|r4lnb2)  # LayerNorm backward block count (GVL_LN_BWD_MAXB builds vs 1024)
     echo "== $v"; grep ln_bwd $O/ln_$v.log
   done
   ;;
+r4lnc)  # LayerNorm backward 512 (shipped) vs 1024 blocks (libgvl_lnb1024.so) inside the steps, same box, alternated
+  for w in qformer lm; do for v in base lnb1024 base lnb1024; do
+    L=$LIBDIR/libgvl_$v.so; [ $v = base ] && L=$LIBDIR/libgvl.so
+    a="--workload qformer --steps 10 --warmup 3"; [ $w = lm ] && a="--steps 2 --warmup 1 --no-secondary"
+    GVL_LIB=$L timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/${w}_$v.json 2> $O/${w}_$v.err; fatal $? bench_$w
+    echo "$w $v $(python -c "import json;d=json.load(open('$O/${w}_$v.json'));print(d['value'],d.get('step_mfma_frac'))")"
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2;;
 esac
