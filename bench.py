@@ -289,11 +289,9 @@ def dominant_kernel(summary, workload="lm", steps=1):
     """Roofline of the GEMM instance with the largest total time.  Durations come from HIP
     events bound to each kernel's own dispatch (gvl.kernels.KernelTimer, dispatch=True):
     the interval rocprofv3's kernel trace reports for the same kernel name.  Also lists the
-    top GEMM instances (per-step launches, average duration, fraction of peak).  The
-    roofline names the dominant gvl kernel; the plain GEMMs gvl_gemm hands to hipBLASLt
-    ("hipblaslt", gemm_lib.cpp) are listed in top_gemms and counted in the totals."""
-    own = {k: v for k, v in summary.items() if k != "hipblaslt"} or summary
-    name, s = max(own.items(), key=lambda kv: kv[1]["ms"])
+    top GEMM instances (per-step launches, average duration, fraction of peak).  Every GEMM
+    is one of libgvl's own kernels (ABI v10: no vendor-library route)."""
+    name, s = max(summary.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = s["ms"] / s["launches"]
     achieved = s["flops"] / (s["ms"] * 1e-3) / 1e12
     top = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:6]

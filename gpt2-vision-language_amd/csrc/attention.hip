@@ -120,6 +120,26 @@ GVL_DEV short8_t load_frag_global(const bf16_t* rowptr, int s, int lane, bool ok
   return __builtin_bit_cast(short8_t, u);
 }
 
+// Max over the four lanes l, l^16, l^32, l^48 that hold one query row (the S fragment's row is
+// spread over the lane groups): two VALU lane swaps (v_permlane16_swap / v_permlane32_swap, no
+// LDS crossbar).  __shfl_xor lowered to ds_bpermute_b32 with an lgkmcnt(0) wait each, i.e. two
+// LDS round trips per query group and key tile on the softmax's critical path.
+#ifndef GVL_ATTN_LDS_SHFL  // 1: the round-4 __shfl_xor form (A/B variant builds only)
+#define GVL_ATTN_LDS_SHFL 0
+#endif
+GVL_DEV float rowmax4(float x) {
+  if (GVL_ATTN_LDS_SHFL) {
+    x = fmaxf(x, __shfl_xor(x, 16, 64));
+    return fmaxf(x, __shfl_xor(x, 32, 64));
+  }
+  const uint32_t u = __float_as_uint(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float y = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const uint32_t v = __float_as_uint(y);
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
   uint4 u = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3]));
   return __builtin_bit_cast(short8_t, u);
@@ -241,8 +261,7 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
       mx = fmaxf(fmaxf(mx, sc[g][2][3]), sc[g][3][0]);
       mx = fmaxf(fmaxf(mx, sc[g][3][1]), sc[g][3][2]);
       mx = fmaxf(mx, sc[g][3][3]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = rowmax4(mx);
 #if GVL_ATTN_FWD_V2
       // deferred rescale (T13): keep the running max while no row's max grew by more than
       // RESCALE_LOG2 (P then stays <= 2^4 before normalisation); rescale O and the row sum
@@ -868,8 +887,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
       mx = fmaxf(fmaxf(mx, sc[g][2][3]), sc[g][3][0]);
       mx = fmaxf(fmaxf(mx, sc[g][3][1]), sc[g][3][2]);
       mx = fmaxf(mx, sc[g][3][3]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = rowmax4(mx);
       constexpr float RESCALE_LOG2 = 4.f;  // deferred rescale, as attn_fwd_kernel
       const float cand = mx * p.c2;
       if (!__all(cand - m[g] <= RESCALE_LOG2)) {

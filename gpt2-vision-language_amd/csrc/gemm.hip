@@ -225,8 +225,13 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 
 }  // namespace
 
+namespace gvl {
+bool pp3_combine_forced() { return env().impl >= 3 && env().cfg == 13; }
+bool w4x_split_forced() { return env().impl >= 3 && env().cfg == 14; }
+}  // namespace gvl
+
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 12, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 14, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -235,18 +240,17 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12)) {
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12 || env().cfg == 14)) {
     GemmP q;
     fill_params(d, q);
-    if (gvl::gemm_w4x_plan(q, d->a_mn, env().cfg == 12)) {
-      snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d, false>", q.bm, d->a_mn ? q.bn : 192,
-               tf[d->a_mn != 0], tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+    if (gvl::gemm_w4x_plan(q, d->a_mn, d->b_mn, env().cfg == 12)) {
+      if (q.splits > 1)
+        snprintf(buf, len, "gemm_w4xs_kernel<%s, %d>", tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+      else
+        snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d, false>", q.bm, d->a_mn ? q.bn : 192,
+                 tf[d->a_mn != 0], tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
       return 0;
     }
-  }
-  if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_routed(d)) {
-    snprintf(buf, len, "hipblaslt");
-    return 0;
   }
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
     GemmP p;
@@ -254,15 +258,15 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     const int cfg = env().cfg;
     if ((cfg < 0 || cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, cfg == 10)) {
       // (cfg 11: default routing with the four-wave kernel off)
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13"};
       if (gvl::gemm_w4d_ok(p))
         snprintf(buf, len, "%s<%s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4dm_kernel" : "gemm_w4d_kernel",
                  tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
       else
         snprintf(buf, len, "%s<3, %s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
-                 tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
+                 tf[d->b_mn != 0], epi[gvl::gemm_w4_epi_kind(p)]);
     } else if (gvl::gemm_pp3_plan(p, cfg == 3 || cfg == 10)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm);
@@ -306,13 +310,9 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GemmP p;
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12) &&
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12 || env().cfg == 14) &&
       gvl::gemm_w4x_try(p, d->a_mn, d->b_mn, env().cfg == 12, s)) {  // AGPR four-wave kernel
     GVL_LAUNCH_CHECK("gvl_gemm(w4x)");
-    return 0;
-  }
-  if (env().impl >= 3 && env().cfg < 0 && gvl::gemm_lib_try(d, s)) {  // plain GEMM on hipBLASLt
-    GVL_LAUNCH_CHECK("gvl_gemm(hipblaslt)");
     return 0;
   }
   if (env().impl >= 3 && gvl::gemm_ring_ok(d)) {
@@ -320,7 +320,7 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
     GemmP q = p;
     if (cfg == 10 && gvl::gemm_w4_plan(p, d->a_mn, true)) {
       gvl::gemm_w4_launch(p, d->b_mn, s);
-    } else if (cfg != 11 && cfg != 3 && cfg != 10 && gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
+    } else if (cfg != 11 && cfg != 13 && cfg != 3 && cfg != 10 && gvl::gemm_w4_try(p, d->a_mn, d->b_mn, s)) {
     } else if (gvl::gemm_pp3_plan(q, cfg == 3 || cfg == 10)) {
       gvl::gemm_pp3_launch(q, d->a_mn, d->b_mn, s);
     } else {

@@ -60,6 +60,10 @@ struct GemmP {
   int32_t ldab[GVL_MAX_GROUP], ldbb[GVL_MAX_GROUP], ldcb[GVL_MAX_GROUP];
   int gtile[GVL_MAX_GROUP + 1];
 };
+// 3152 B with 48 problems.  A kernel reads its arguments by scalar loads of the fields it uses,
+// so the per-problem tables cost the launches that never touch them only the host-side copy of
+// the block (graph replays re-use the captured copy); the bound keeps it clear of the 4 KiB limit.
+static_assert(sizeof(GemmP) <= 3584, "GemmP must stay well inside the 4 KiB kernel-argument limit");
 
 // Work item -> (split, tile row, tile col).  Workgroups are first remapped so that each
 // XCD (blockIdx % 8) owns a contiguous range of work items, then that range is walked in
@@ -195,9 +199,14 @@ enum {
   EPI_BIAS_ACT_D = 9, EPI_BIAS_ACT_ERF_D = 10, EPI_MUL = 11,
   // C = residual + dropout(AB + bias): the Q-Former out_proj / MLP output branches
   // (gpt2_q_former/model.py:139-145, q += drop(...)), mask = the counter hash of (m, n)
-  EPI_BIAS_DROP_RES = 12
+  EPI_BIAS_DROP_RES = 12,
+  // C = residual + tanh(gate) * (AB + bias), the un-gated branch AB + bias stored to pre_out for
+  // the gate gradient: the cross-att decoder's xattn.c_proj (gpt2_cross-att/model.py:57,99-101).
+  // Only the four-wave kernels take it (gemm_w4.hip, gemm_w4_epi_kind); gemm_epi_kind still
+  // answers EPI_GEN for a gated GEMM, so no other kernel family sees this kind
+  EPI_GATE_RES = 13
 };
-constexpr int EPI_KINDS = 13;
+constexpr int EPI_KINDS = 14;
 
 template <int EPI>
 struct EpiKind {
@@ -207,8 +216,10 @@ struct EpiKind {
   static constexpr bool DACT = EPI == EPI_DACT || EPI == EPI_DACT_ERF || MUL;
   static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF || EPI == EPI_BIAS_ACT_ERF_D;
   static constexpr bool DROP = EPI == EPI_BIAS_DROP_RES;
-  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT || DROP;
-  static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES || DROP;
+  static constexpr bool GATE = EPI == EPI_GATE_RES;
+  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT || DROP || GATE;
+  static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES || DROP || GATE;
+  static constexpr bool PRE_OUT = ACT || GATE;  // stores a bf16 [M, N] side output (pre_out)
   static constexpr bool AUX = DACT || RES;  // reads a bf16 [M, N] operand (pre_in / residual)
 };
 
@@ -228,9 +239,11 @@ struct EpiPre {
   static constexpr int XH = FULL ? FM : FM / 2;  // else half a tile at a time, in the epilogue
   uint2 x[KD::AUX ? XH : 1][KD::AUX ? FN : 1];
   uint64_t seed = 0;  // effective dropout seed (DROP), read with the bias, not per element
+  float gatev = 1.f;  // tanh(gate) (GATE), read with the bias
   bool pre0 = false;  // the first half (fragment rows 0 .. XH-1) was fetched ahead of the epilogue
   GVL_DEV void load_bias(const GemmP& p, int64_t nw0, int lane) {
     if constexpr (KD::DROP) seed = seed_eff(p.seed, p.seed_ptr);
+    if constexpr (KD::GATE) gatev = tanhf(bf2f(*p.gate));
     if constexpr (KD::BIAS) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -298,6 +311,13 @@ static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t 
       for (int r = 0; r < 4; ++r)
         v[r] = rng_keep(seed, base + r, p.drop_thresh) ? v[r] * p.drop_scale : 0.f;
     }
+    if constexpr (KD::GATE) {  // the caller stores pre (the un-gated branch) with 16-B stores
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pre[r] = v[r];
+        v[r] *= gatev;
+      }
+    }
     if constexpr (KD::RES) {
       v[0] += lo_bf(ax.x); v[1] += hi_bf(ax.x); v[2] += lo_bf(ax.y); v[3] += hi_bf(ax.y);
     }
@@ -331,6 +351,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
   bf16_t* const cbase = reinterpret_cast<bf16_t*>(cout ? cout : p.C);
   float gatev = 1.f;
   if constexpr (EPI == EPI_GEN) gatev = p.gate ? tanhf(bf2f(*p.gate)) : 1.f;
+  if constexpr (EpiKind<EPI>::GATE) gatev = pre.gatev;
   const bool plain = EPI == EPI_PLAIN ||
                      (EPI == EPI_GEN && !p.bias && !p.dact && !p.act && !p.has_drop && !p.gate &&
                       !p.residual);
@@ -363,7 +384,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         if (mok && n1 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j + 1], m, n1, alpha, gatev, b1, a1, v1, h1, pre.seed);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
         x1 = pack2(v1[0], v1[1]); y1 = pack2(v1[2], v1[3]);
-        if (KD::ACT && p.pre_out) {  // pre-activation: same lane swap, 16-B stores
+        if (KD::PRE_OUT && p.pre_out) {  // pre-activation / un-gated branch: same lane swap, 16-B stores
           const auto hx = __builtin_amdgcn_permlane16_swap(pack2(h0[0], h0[1]), pack2(h1[0], h1[1]),
                                                            false, false);
           const auto hy = __builtin_amdgcn_permlane16_swap(pack2(h0[2], h0[3]), pack2(h1[2], h1[3]),
@@ -394,7 +415,7 @@ GVL_DEV void gemm_epilogue16(const GemmP& p, const float4_t (&acc)[FM][FN], int6
         const uint2 a0 = KD::AUX ? pre.x[KD::AUX ? i % XH : 0][KD::AUX ? j : 0] : make_uint2(0, 0);
         if (mok && n0 < p.N) gemm_epi_vals_k<EPI>(p, acc[i][j], m, n0, alpha, gatev, b0, a0, v0, h0, pre.seed);
         x0 = pack2(v0[0], v0[1]); y0 = pack2(v0[2], v0[3]);
-        if (KD::ACT && p.pre_out && mok && n0 < p.N)
+        if (KD::PRE_OUT && p.pre_out && mok && n0 < p.N)
           *reinterpret_cast<uint2*>(p.pre_out + m * p.ldp + n0) =
               make_uint2(pack2(h0[0], h0[1]), pack2(h0[2], h0[3]));
       }
@@ -501,6 +522,8 @@ int gemm_ring_pick(int64_t M, int64_t N, int64_t K, int forced, int a_mn);
 int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels (gemm_plan.hip)
 bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
+bool pp3_combine_forced();  // gemm.hip: gvl_gemm_tune(3, 13) (the persistent kernel's combine, tests)
+bool w4x_split_forced();    // gemm.hip: gvl_gemm_tune(3, 14) (the AGPR kernel's K split, tests)
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
 int gemm_pp3_launch_ff(const GemmP& p, hipStream_t s);  // gemm_pp3_{ff,ft,tf,tt}.hip
 int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);
@@ -510,12 +533,11 @@ int gemm_pp3_splits(int64_t M, int64_t N, int64_t K, int gran = 32);
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_rows128(const GemmP& p);  // the launch uses 128-row tiles (gemm_w4m_kernel)
+int gemm_w4_epi_kind(const GemmP& p);  // gemm_epi_kind + EPI_GATE_RES (four-wave kernels only)
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 bool gemm_w4d_ok(const GemmP& p);  // gemm_w4d.hip: direct-A variant for a w4-planned shape
-bool gemm_lib_routed(const gvl_gemm_desc* d);         // gemm_lib.cpp: plain GEMM for hipBLASLt
-bool gemm_lib_try(const gvl_gemm_desc* d, hipStream_t s);  // launched there (else false)
 int gemm_w4d_launch(const GemmP& p, int b_mn, bool rows128, hipStream_t s);
-bool gemm_w4x_plan(GemmP& p, int a_mn, bool force);  // gemm_w4x.hip: AGPR four-wave kernel
+bool gemm_w4x_plan(GemmP& p, int a_mn, int b_mn, bool force);  // gemm_w4x.hip: AGPR four-wave kernel
 bool gemm_w4x_try(const GemmP& p, int a_mn, int b_mn, bool force, hipStream_t s);
 bool gemm_w4x_batched_try(const GemmP& p, hipStream_t s);  // batched dW (a_mn, b_mn, C += AB)
 bool w4x_dw_plan(GemmP& p);  // its tile choice (bm / bn / tiles), false when not routed

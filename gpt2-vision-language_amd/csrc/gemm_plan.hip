@@ -148,7 +148,15 @@ bool gemm_pp3_plan(GemmP& p, bool force, int gran) {
   p.bm = 256;
   int sp = 1;
   if (p.ws != nullptr) sp = gemm_pp3_splits(p.M, p.N, p.K, gran);
-  if (sp <= 2 && p.ws != nullptr && p.tickets != nullptr && gemm_epi_kind(p) != EPI_GEN) {
+  // the persistent kernel's in-launch two-way combine for single GEMMs: measured slower than
+  // whole-K tiles, so only with GVL_PP3_COMBINE=1, whatever tickets the caller passes
+  // (since round 5 gvl.kernels always passes them, for the AGPR kernel's split, gemm_w4x.hip)
+  static const bool combine_env = [] {
+    const char* e = getenv("GVL_PP3_COMBINE");
+    return e && e[0] == '1';
+  }();
+  const bool combine_on = combine_env || pp3_combine_forced();  // (gvl_gemm_tune(3, 13): tests)
+  if (sp <= 2 && combine_on && p.ws != nullptr && p.tickets != nullptr && gemm_epi_kind(p) != EPI_GEN) {
     p.bn = 256;
     pp3_choose_combined(p, gran);
     if (force) return true;

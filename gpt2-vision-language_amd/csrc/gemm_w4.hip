@@ -431,7 +431,7 @@ int launch_w4(const GemmP& p, hipStream_t s) {
 
 template <bool BMN>
 int launch_w4_epi(const GemmP& p, hipStream_t s) {
-  switch (gvl::gemm_epi_kind(p)) {
+  switch (gvl::gemm_w4_epi_kind(p)) {
     case EPI_PLAIN: return launch_w4<BMN, EPI_PLAIN>(p, s);
     case EPI_BIAS: return launch_w4<BMN, EPI_BIAS>(p, s);
     case EPI_BIAS_RES: return launch_w4<BMN, EPI_BIAS_RES>(p, s);
@@ -444,6 +444,7 @@ int launch_w4_epi(const GemmP& p, hipStream_t s) {
     case EPI_BIAS_ACT_ERF_D: return launch_w4<BMN, EPI_BIAS_ACT_ERF_D>(p, s);
     case EPI_MUL: return launch_w4<BMN, EPI_MUL>(p, s);
     case EPI_BIAS_DROP_RES: return launch_w4<BMN, EPI_BIAS_DROP_RES>(p, s);
+    case EPI_GATE_RES: return launch_w4<BMN, EPI_GATE_RES>(p, s);
     default: return -1;
   }
 }
@@ -461,12 +462,28 @@ int w4_mode() {
 
 namespace gvl {
 
+// The four-wave kernels' epilogue kind: gemm_epi_kind, plus the gated residual (EPI_GATE_RES:
+// bias, residual, gate and the un-gated branch stored to pre_out; no dropout / activation) that
+// every other family runs on the generic epilogue.  Before round 5 the cross-att decoder's 12
+// gated xattn.c_proj GEMMs per step (3968 x 768 x 768) fell to the 128 x 128 ring kernel's
+// runtime-flag epilogue for that reason: 32 us each, 0.058 of peak.
+int gemm_w4_epi_kind(const GemmP& p) {
+  static const bool gate_on = [] {  // GVL_W4_GATE=0: the generic path as before (A/B)
+    const char* e = getenv("GVL_W4_GATE");
+    return !(e && e[0] == '0');
+  }();
+  if (gate_on && p.gate && p.bias && p.residual && p.pre_out && !p.has_drop && !p.c_f32 && !p.act &&
+      !p.dact)
+    return EPI_GATE_RES;
+  return gemm_epi_kind(p);
+}
+
 // Shapes it takes by default: narrow outputs (N <= 1024) whose 256x256 tiling leaves most CUs
 // idle and whose 192x128 tiling fills at least half the chip.
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
   if (a_mn || p.c_f32 || p.K % (6 * KS) != 0 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
-  if (gemm_epi_kind(p) == EPI_GEN) return false;
+  if (gemm_w4_epi_kind(p) == EPI_GEN) return false;
   if (force || w4_mode() == 2) return true;
   if (w4_mode() == 0) return false;
   // GVL_W4=3 (A/B): also the short-K wide outputs (K <= 1024, N <= 4096: c_attn / c_fc

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 9  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 10  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -76,7 +76,6 @@ SIGNATURES = {
     "gvl_gemm_tune": (C.c_int, [c_i32, c_i32]),
     "gvl_gemm_kernel_name": (C.c_int, [C.POINTER(GemmDesc), C.c_char_p, c_i32]),
     "gvl_gemm_batched_kernel_name": (C.c_int, [C.c_char_p, c_i32]),
-    "gvl_gemm_lib_route": (C.c_int, [c_i32]),
     "gvl_layernorm_fwd": (C.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                     c_i64, c_i64, c_f32, c_vp]),
     "gvl_layernorm_bwd_workspace_size": (c_i64, [c_i64, c_i64]),

@@ -723,6 +723,7 @@ class MHAFn(torch.autograd.Function):
         # (one grouped launch at the end of backward; the grad-ready hook after the last slice)
         dfw = sw is not None and DEFER_BRIDGE and DEFER_INPROJ and DEFER_WGRAD
         dfb = sb is not None and DEFER_BRIDGE and DEFER_INPROJ and DEFER_WGRAD
+        b_deferred = [False]  # some slice went to the queue: its flush fires the grad-ready hook
 
         def wg(dy_, x_, rows):
             if dfw:
@@ -731,8 +732,11 @@ class MHAFn(torch.autograd.Function):
                 K.linear_dw(dy_, x_, out=tw[rows], residual=tw[rows] if sw is not None else None)
 
         def bg(dy_, rows):
-            if dfb:  # (dqkv / dqp / dkvp: fresh contiguous buffers)
+            # deferred under the same guard as _bgrad (rows present, unit column stride); today
+            # dqkv / dqp / dkvp are fresh contiguous buffers, so the guard only protects callers
+            if dfb and dy_.shape[0] > 0 and dy_.stride(1) == 1:
                 _defer_wgrad(P_in_b, tb[rows], dy_, None)
+                b_deferred[0] = True
             elif tb is not None:
                 K.colsum(dy_, out=tb[rows], accumulate=sb is not None)
 
@@ -767,7 +771,7 @@ class MHAFn(torch.autograd.Function):
                 dkv_in = K.linear_dx(dkvp, in_w[C:]).view(B, Tk, C)
         if sw is not None and not dfw:
             _ready(P_in_w)
-        if sb is not None and not dfb:
+        if sb is not None and not b_deferred[0]:
             _ready(P_in_b)
         return dq_in, dkv_in, din_w, din_b, d_out_w, d_out_b, dres, None, None, None, None, None
 

@@ -99,9 +99,9 @@ def _gemm_workspace(device):
 
 _TK = {}
 GEMM_TICKETS = 1 << 16
-# In-launch two-way split-K combine (gvl.h ABI v5 tickets): measured slower than whole-K
-# tiles on the caption step's N = 768 GEMMs, so off unless GVL_PP3_COMBINE=1.
-SPLIT_COMBINE = os.environ.get("GVL_PP3_COMBINE", "0") == "1"
+# Arrival tickets (gvl.h ABI v5) go with every gvl_gemm call: the AGPR four-wave kernel's
+# in-launch K split of the caption decoders' N = 768 products uses them (gemm_w4x.hip); the
+# persistent kernel's own two-way combine stays off unless GVL_PP3_COMBINE=1 (checked in C).
 # Batched weight gradients may use it (gvl_gemm_batched decides; GVL_BATCHED_SPLIT=0: never).
 BATCHED_SPLIT = os.environ.get("GVL_BATCHED_SPLIT", "1") != "0"
 
@@ -173,9 +173,8 @@ def gemm(a, b, *, a_mn=False, b_mn=False, out=None, alpha=1.0, alpha_ptr=None, b
     d.c_fp32 = int(out.dtype == F32)
     ws = _gemm_workspace(a.device)
     d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
-    if SPLIT_COMBINE:
-        tk = _gemm_tickets(a.device)
-        d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
+    tk = _gemm_tickets(a.device)
+    d.tickets, d.ticket_count = tk.data_ptr(), tk.numel()
     if _timer is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 9
+#define GVL_ABI_VERSION 10
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -124,7 +124,11 @@ int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
  * 128x128 tiles, direct-A where K % 384 == 0) where they apply, 11 = default routing without
  * them (and without the AGPR four-wave kernel), 12 (ABI v8, round 4) the AGPR four-wave kernel
  * (gemm_w4x.hip: 256 x 192 / 128 x 192 tiles, K-contiguous A, plain or bias + residual) where
- * it applies; other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase
+ * it applies; 13 (ABI v10) = cfg 11 with the persistent kernel's in-launch two-way combine
+ * enabled for single GEMMs (tests; otherwise only with env GVL_PP3_COMBINE=1, since the caller's
+ * tickets now also serve the AGPR kernel's split); 14 (ABI v10) = default routing with the AGPR
+ * kernel's in-launch K split of the caption decoders' N = 768 products (gemm_w4xs_kernel; off by
+ * default, env GVL_W4X_SPLIT=1); other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase
  * kernel) is rejected. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a
@@ -134,12 +138,8 @@ int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len);
  * gvl_gemm_batched_dbias call launched as one batched launch ("" when it ran the problems one
  * by one through gvl_gemm): the bench attributes the batched weight-gradient launches too. */
 int gvl_gemm_batched_kernel_name(char* buf, int32_t len);
-/* ABI v8: plain GEMMs (no bias / activation / residual / dropout / gate / alpha_ptr, bf16 C)
- * of the shapes where hipBLASLt's kernel is measured faster (N = 768 with 768 <= K <= 4096,
- * M >= 4096) run on hipBLASLt from inside gvl_gemm (impl 3, cfg -1);
- * gvl_gemm_kernel_name reports "hipblaslt" for them.  mode 0 = never, 1 = those shapes
- * (default; env GVL_GEMM_LIB), 2 = every plain GEMM (tests).  Returns the previous mode. */
-int gvl_gemm_lib_route(int32_t mode);
+/* (ABI v8-v9 had gvl_gemm_lib_route: plain N = 768 GEMMs handed to hipBLASLt.  Removed in
+ * ABI v10: every GEMM runs on libgvl's own kernels; libgvl links no vendor BLAS.) */
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim (eps given; reference uses 1e-5).

@@ -27,14 +27,24 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     lib.gvl_abi_version.restype = ctypes.c_int
-    assert lib.gvl_abi_version() == 9
+    assert lib.gvl_abi_version() == 10
+
+
+def test_library_links_no_vendor_blas():
+    """Since ABI v10 every GEMM runs on libgvl's own kernels: the library has no hipBLASLt /
+    rocBLAS dependency (round 4's gvl_gemm_lib_route is gone)."""
+    import subprocess
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-d", LIB], capture_output=True,
+                         text=True, check=True).stdout
+    needed = [ln for ln in out.splitlines() if "NEEDED" in ln]
+    assert needed and not any("blas" in ln.lower() for ln in needed), needed
 
 
 def test_binding_covers_header():
     from gvl import _lib
     assert sorted(_lib.SIGNATURES) == declared()
     lib = _lib.load()  # binds every symbol with its argtypes
-    assert lib.gvl_abi_version() == 9
+    assert lib.gvl_abi_version() == 10
 
 
 def test_rejects_bad_arguments_without_gpu():

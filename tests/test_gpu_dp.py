@@ -274,6 +274,8 @@ def test_two_ranks_gloo_match_single_process(cuda, kind, graphed):
     # eager: both losses are computed before any update from identical weights, so they differ
     # only by the order of the bf16/fp32 reductions; the graphed step's loss is the replay's,
     # i.e. after the warm-up step's update, whose Adam-normalised gradient noise moves it more
-    assert lrel < (2e-3 if graphed else 1e-5), lrel
-    assert nrel < (3e-2 if graphed else 1e-2), nrel
+    # bounds ~10x the measured margins (profiles/r4/parity_margins_r4fin3.json: graphed loss
+    # 9.0e-6 / 1.2e-5, norm 3.0e-4 / 8.3e-4 for the LM / Q-Former)
+    assert lrel < (1.5e-4 if graphed else 1e-5), lrel
+    assert nrel < (1e-2 if graphed else 1e-2), nrel
     assert worst[0] < (2e-2 if graphed else 1e-2), worst

@@ -22,22 +22,6 @@ def _k():
     return K
 
 
-@pytest.fixture(autouse=True)
-def _own_gemm_kernels(request):
-    """The tests here exercise gvl's own GEMM kernels, so the plain GEMMs that gvl_gemm routes
-    to hipBLASLt by default (gemm_lib.cpp) run on them (gvl_gemm_lib_route(0)), except in
-    test_gemm_library_route*, which covers the routed path."""
-    if request.node.name.startswith("test_gemm_library_route"):
-        yield
-        return
-    from gvl import _lib
-    prev = _lib.lib().gvl_gemm_lib_route(0)
-    try:
-        yield
-    finally:
-        _lib.lib().gvl_gemm_lib_route(prev)
-
-
 def _r(t):
     """round to bf16, back to fp32 CPU"""
     return t.to(BF).float().cpu()
@@ -178,7 +162,9 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
         d.dact, d.pre_in, d.ldp = {"mul": 3, "dact": 1, "dact_erf": 2}[epi], p, N
     if epi == "drop_res":
         d.drop_p, d.seed = 0.1, 1
-    if tickets:  # as gvl.kernels.gemm passes them (workspace + in-launch combine tickets)
+    if epi == "gate_res":
+        d.bias, d.residual, d.ldr, d.gate, d.pre_out, d.ldp = p, p, N, p, p, N
+    if True:  # as gvl.kernels.gemm passes them (workspace + in-launch combine tickets, always)
         K_ = _k()
         ws, tk = K_._gemm_workspace(A.device), K_._gemm_tickets(A.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
@@ -188,10 +174,11 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
-@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 4096, 0, 0)])
-def test_gemm_library_route(cuda, M, N, K, a_mn, b_mn):
-    """Plain GEMMs of the shapes measured faster on hipBLASLt (gemm_lib.cpp: the caption
-    decoder's c_fc.dX) run there from inside gvl_gemm; fused ones never do.  vs the fp32
+@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 4096, 0, 0),
+                                               (4096, 768, 3072, 0, 1)])
+def test_gemm_caption_dx_on_own_kernels(cuda, M, N, K, a_mn, b_mn):
+    """The plain N = 768 products that round 4 handed to hipBLASLt (the caption decoder's and the
+    Q-Former MLP's c_fc.dX) run on libgvl's four-wave kernels since ABI v10: vs the fp32
     product, with alpha, and replayed from a captured hipGraph."""
     K_ = _k()
     torch.manual_seed(M + N + K)
@@ -199,13 +186,12 @@ def test_gemm_library_route(cuda, M, N, K, a_mn, b_mn):
     b = (torch.randn(K, N) * 0.05).to(BF)
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
-    assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="plain") == "hipblaslt"
-    assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="bias") != "hipblaslt"
+    assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="plain").startswith("gemm_w4")
     ref = a.float() @ b.float()
     y = K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), alpha=0.5)
     assert rel_err(y.float().cpu().numpy(), 0.5 * ref.numpy()) < 8e-3
     out = torch.empty(M, N, dtype=BF, device=cuda)
-    K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=out)  # warm (plan built outside capture)
+    K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=out)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=out)
@@ -216,26 +202,20 @@ def test_gemm_library_route(cuda, M, N, K, a_mn, b_mn):
 
 
 @pytest.mark.parametrize("a_mn,b_mn", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_library_route_layouts(cuda, a_mn, b_mn):
-    """Every operand layout and ragged sizes through the hipBLASLt route (mode 2: every plain
-    GEMM), including a strided output view."""
-    from gvl import _lib
+def test_gemm_strided_output_view(cuda, a_mn, b_mn):
+    """Every operand layout with ragged sizes into a strided output view: the columns past N
+    are never written."""
     K_ = _k()
-    prev = _lib.lib().gvl_gemm_lib_route(2)
-    try:
-        M, N, K = 1000, 776, 160
-        torch.manual_seed(a_mn * 2 + b_mn)
-        a = torch.randn(M, K).to(BF)
-        b = torch.randn(K, N).to(BF)
-        A = (a.t().contiguous() if a_mn else a).to(cuda)
-        B = (b if b_mn else b.t().contiguous()).to(cuda)
-        assert _kernel_name(A, B, a_mn, b_mn, M, N, K, epi="plain") == "hipblaslt"
-        big = torch.full((M, N + 8), 7.0, dtype=BF, device=cuda)
-        K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=big[:, :N])
-        assert rel_err(big[:, :N].float().cpu().numpy(), (a.float() @ b.float()).numpy()) < 8e-3
-        assert torch.all(big[:, N:] == 7.0)
-    finally:
-        _lib.lib().gvl_gemm_lib_route(prev)
+    M, N, K = 1000, 776, 160
+    torch.manual_seed(a_mn * 2 + b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = torch.randn(K, N).to(BF)
+    A = (a.t().contiguous() if a_mn else a).to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    big = torch.full((M, N + 8), 7.0, dtype=BF, device=cuda)
+    K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), out=big[:, :N])
+    assert rel_err(big[:, :N].float().cpu().numpy(), (a.float() @ b.float()).numpy()) < 8e-3
+    assert torch.all(big[:, N:] == 7.0)
 
 
 @pytest.mark.parametrize("b_mn", [0, 1])
@@ -260,7 +240,7 @@ def test_gemm_w4x(cuda, b_mn, epi, M, N, K):
     h = a.float() @ b.float()
     _lib.lib().gvl_gemm_tune(3, 12)
     try:
-        assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x_kernel")
+        assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x")
         big = torch.full((M + 3, N + 8), 7.0, dtype=BF, device=cuda)
         out = big[:M, :N]
         if epi == "plain":
@@ -277,6 +257,56 @@ def test_gemm_w4x(cuda, b_mn, epi, M, N, K):
         assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x_kernel")
     assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
     assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
+
+
+@pytest.mark.parametrize("M,N,K,b_mn,epi,S", [
+    (8064, 768, 3072, 1, "plain", 2), (8064, 768, 3072, 0, "bias_res", 2),
+    (8064, 768, 768, 0, "bias_res", 2), (8064, 768, 2304, 1, "plain", 2),
+    (8192, 768, 3072, 1, "plain", 2), (8000, 768, 384, 0, "plain", 2)])
+def test_gemm_w4x_split(cuda, M, N, K, b_mn, epi, S):
+    """The AGPR four-wave kernel's in-launch K split (gemm_w4xs_kernel, round 5): the caption
+    decoders' and the Q-Former's N = 768 products as S K-slices per 256 x 192 tile meeting in
+    the launch.  Chosen by default at these shapes (checked by name); vs the fp32 product; the
+    slices are summed in split order, so two runs are bit-identical; the arrival counters are
+    left zero; replayed from a captured hipGraph; ragged M (the last tile row part-empty)."""
+    from gvl import _lib
+    K_ = _k()
+    torch.manual_seed(M + N + K + b_mn + S)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = a.to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    _lib.lib().gvl_gemm_tune(3, 14)  # the split is off by default (DESIGN, round 5)
+    try:
+        _run_w4x_split(K_, A, B, a, b, M, N, K, b_mn, epi, cuda)
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+
+
+def _run_w4x_split(K_, A, B, a, b, M, N, K, b_mn, epi, cuda):
+    assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi) == f"gemm_w4xs_kernel<{'true' if b_mn else 'false'}, " \
+        f"{0 if epi == 'plain' else 2}>"
+    h = a.float() @ b.float()
+    kw, ref = {}, h
+    if epi == "bias_res":
+        bias, res = torch.randn(N).to(BF), torch.randn(M, N).to(BF)
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    big = torch.full((M + 3, N + 8), 7.0, dtype=BF, device=cuda)
+    out = big[:M, :N]
+    outs = []
+    for _ in range(2):
+        K_.gemm(A, B, b_mn=bool(b_mn), out=out, **kw)
+        outs.append(out.clone())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        K_.gemm(A, B, b_mn=bool(b_mn), out=out, **kw)
+    out.fill_(0.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert rel_err(outs[0].float().cpu().numpy(), ref.numpy()) < 8e-3
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
+    assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
+    assert int(K_._gemm_tickets(A.device).abs().sum()) == 0
 
 
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])
@@ -429,7 +459,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
     from gvl import _lib
-    _lib.lib().gvl_gemm_tune(3, 11)  # default routing minus the four-wave kernel (gemm_w4)
+    _lib.lib().gvl_gemm_tune(3, 13)  # default routing minus the four-wave kernels, pp3 combine on
     try:
         name = _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=True)
     finally:
@@ -458,8 +488,7 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
         O.gelu_erf(hx).sum().backward()
         kw, ref = dict(dact=2, pre_in=hpre.to(cuda)), h * hx.grad
     outs = []
-    K_.SPLIT_COMBINE = True
-    _lib.lib().gvl_gemm_tune(3, 11)
+    _lib.lib().gvl_gemm_tune(3, 13)
     try:
         for _ in range(2):
             if epi == "res_inplace":
@@ -467,7 +496,6 @@ def test_gemm_splitk_combined_in_launch(cuda, a_mn, b_mn, epi, M, N, K):
                 kw = dict(residual=acc, out=acc)
             outs.append(K_.gemm(A, B, a_mn=bool(a_mn), b_mn=bool(b_mn), **kw))
     finally:
-        K_.SPLIT_COMBINE = False
         _lib.lib().gvl_gemm_tune(3, -1)
     torch.cuda.synchronize()
     assert rel_err(outs[0].float().cpu().numpy(), ref.detach().numpy()) < 8e-3
@@ -491,8 +519,12 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
     name = _kernel_name(A, B, a_mn, b_mn, M, N, K, epi=epi)
-    if not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
+    if not a_mn and os.environ.get("GVL_W4X_SPLIT") == "1" and _w4xs_name(M, N, K, b_mn, epi):
+        assert name == _w4xs_name(M, N, K, b_mn, epi), name  # (the AGPR kernel's K split, A/B)
+    elif not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
         assert name.startswith(_w4_name(M, K, epi)), name
+    elif a_mn and K >= 3072:  # with gvl.kernels' workspace the planner splits K: 128x128 ring
+        assert name.startswith("gemm_ring_kernel") or name.endswith(", 192, 128>"), name
     else:
         assert name.startswith("gemm_pp3_kernel") and name.endswith(", 192, 128>"), name
     h = a.float() @ b.float()
@@ -526,6 +558,22 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
 
 # epilogues gemm_w4d_kernel is instantiated for (gemm_w4d.h epi_supported)
 W4D_EPIS = ("plain", "bias", "bias_res", "res_inplace", "drop_res")
+
+
+def _w4xs_name(M, N, K, b_mn, epi):
+    """The AGPR kernel's in-launch K split (gemm_w4x.hip w4x_split_plan) for this
+    K-contiguous-A shape when the split is on (GVL_W4X_SPLIT=1 / gvl_gemm_tune(3, 14)), else None."""
+    if N != 768:
+        return None
+    if not (epi == "plain" or (epi == "bias_res" and not b_mn)):
+        return None
+    tiles = (M + 255) // 256 * 4
+    S = 1
+    while tiles * S * 2 <= 256 and S < 2:
+        S *= 2
+    if S == 1 or tiles * S * 10 < 256 * 9 or K % (32 * S) or K // S < 192:
+        return None
+    return f"gemm_w4xs_kernel<{'true' if b_mn else 'false'}, {0 if epi == 'plain' else 2}>"
 
 
 def _w4_name(M, K, epi):
@@ -593,6 +641,38 @@ def test_gemm_w4(cuda, b_mn, epi, M, N, K):
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,force", [(3968, 768, 768, False), (3970, 776, 192, True),
+                                         (300, 128, 192, True), (8064, 768, 768, True)])
+def test_gemm_w4_gated_residual(cuda, M, N, K, force):
+    """y = residual + tanh(gate) * (x W^T + b) with the un-gated branch stored (EPI_GATE_RES,
+    gemm_w4.hip): the cross-att decoder's xattn.c_proj (gpt2_cross-att/model.py:57,99-101).  At
+    its shape (3968 x 768 x 768) the default routing takes the 128-row four-wave kernel (round 4:
+    the generic-epilogue ring kernel); forced on ragged M / N, a sub-chip grid and 192-row tiles."""
+    from gvl import _lib
+    K_ = _k()
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(N, K) * 0.05).to(BF)
+    bias = torch.randn(N).to(BF)
+    res = torch.randn(M, N).to(BF)
+    gate = torch.tensor(-0.45).to(BF)
+    ybr = torch.full((M, N), float("nan"), dtype=BF, device=cuda)
+    A, B = x.to(cuda), w.to(cuda)
+    if force:
+        _lib.lib().gvl_gemm_tune(3, 10)
+    try:
+        name = _kernel_name(A, B, 0, 0, M, N, K, epi="gate_res")
+        y = K_.gemm(A, B, bias=bias.to(cuda), residual=res.to(cuda), gate=gate.to(cuda), pre_out=ybr)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().gvl_gemm_tune(3, -1)
+    assert "gemm_w4" in name and name.endswith(", 13>"), name
+    h = x.float() @ w.float().t() + bias.float()
+    ref = res.float() + math.tanh(float(gate.float())) * h
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+    assert rel_err(ybr.float().cpu().numpy(), h.numpy()) < 8e-3
 
 
 @pytest.mark.parametrize("a_mn,b_mn,M,N,K", [(1, 1, 768, 768, 8192), (0, 1, 256, 512, 4096),
@@ -817,7 +897,10 @@ def test_gemm_batched_wgrad(cuda, count, M, N, K, acc):
     + [(4096, 2304, 768)] * 2 + [(4096, 768, 768)] * 2 + [(4224, 1536, 768)] * 2,
     # an LM backward flush (12 blocks x c_attn / attn.c_proj / c_fc / mlp.c_proj, 48 problems,
     # the GVL_MAX_GROUP limit) at 1024 of its 16384 tokens
-    [(1024, 768, 3072), (1024, 3072, 768), (1024, 768, 768), (1024, 2304, 768)] * 12])
+    [(1024, 768, 3072), (1024, 3072, 768), (1024, 768, 768), (1024, 2304, 768)] * 12,
+    # one problem: its bias sum is fused too (a grouped launch of one problem used to
+    # skip the Db update while reporting success)
+    [(4096, 768, 3072)]])
 def test_gemm_grouped_wgrad(cuda, shapes):
     """gvl_gemm_grouped: weight gradients of different shapes (the Q-Former bridge's deferred
     out_proj / MLP / projection dW at K = 4096 / 4224 tokens, plus a ragged 200 x 136 one over

@@ -18,5 +18,5 @@ OBJS=""
 for o in $B/*.o; do
   base=$(basename $o); [ -f $V/$base ] && OBJS="$OBJS $V/$base" || OBJS="$OBJS $o"
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/gpt2-vision-language_amd/gvl/libgvl_$NAME.so $OBJS -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/gpt2-vision-language_amd/gvl/libgvl_$NAME.so $OBJS
 echo built libgvl_$NAME.so

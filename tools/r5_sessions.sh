@@ -1,0 +1,62 @@
+#!/bin/bash
+# Round-5 GPU sessions (run on the GPU box through gpurun): bash tools/r5_sessions.sh <name>.
+# Every GPU step has its own time limit; a session stops at the first failing step.
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; S=${1:?session}; O=gpurun_out/$S; mkdir -p $O
+LIBDIR=gpt2-vision-language_amd/gvl
+fatal() { [ "$1" -eq 0 ] || { echo "fatal rc $1 at $2"; exit $1; }; }
+suite() {  # GPU suite (margins recorded) + smoke
+  GVL_MARGINS_DIR=$O/parity_margins timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf \
+    --timeout 300 --timeout-method thread -p no:cacheprovider > $O/suite.log 2>&1
+  rc=$?; echo "suite rc=$rc"; tail -3 $O/suite.log; fatal $rc suite
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc $(tail -1 $O/smoke.log)"; fatal $rc smoke
+}
+ktests() {  # ktests <log> <pytest -k expression> [file]
+  timeout -k 10 600 python -u -m pytest ${3:-tests/test_gpu_kernels.py} -q -x -k "$2" --timeout 300 \
+    --timeout-method thread -p no:cacheprovider > $O/$1.log 2>&1; rc=$?; echo "$1: $(tail -1 $O/$1.log)"; fatal $rc $1
+}
+diag() {  # diag <tag> <M> <set> <cols>   (env passes through)
+  GVL_DIAG_COLS=$4 timeout -k 10 240 python -u tools/gemm_diag.py $2 $3 > $O/diag_$1_$2_$3.log 2>&1
+  rc=$?; echo "== $1 M=$2 $3"; grep "N=" $O/diag_$1_$2_$3.log; fatal $rc diag
+}
+bench() {  # bench <tag> <workload> [steps]   (env passes through)
+  local a="--workload $2 --steps ${3:-10} --warmup 3"; [ $2 = lm ] && a="--steps ${3:-2} --warmup 1 --no-secondary"
+  timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/$1.json 2> $O/$1.err; fatal $? bench_$1
+  echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'))")"
+}
+case $S in
+r5a)  # gated four-wave epilogue (cross-att xattn.c_proj), grouped single problem, hipBLASLt-off A/B
+  [ -n "$SKIP_KT" ] || ktests kt "w4_gated or grouped_wgrad or gemm_dropout_gate or test_gemm_w4x"
+  ktests dp "two_ranks" tests/test_gpu_dp.py
+  for r in 1 2; do for g in 1 0; do GVL_W4_GATE=$g bench cross_g${g}_$r cross; done; done
+  for r in 1 2; do
+    bench qf_lib1_$r qformer
+    GVL_GEMM_LIB=0 bench qf_lib0_$r qformer
+    GVL_GEMM_LIB=0 GVL_W4X_128=1 bench qf_lib0x128_$r qformer
+  done
+  for M in 8064 4096; do
+    diag lib1 $M narrow all
+    GVL_GEMM_LIB=0 diag lib0 $M narrow epi
+    GVL_GEMM_LIB=0 GVL_W4X_128=1 diag lib0x128 $M narrow epi
+  done
+  ;;
+r5b)  # hipBLASLt gone (ABI v10), AGPR kernel's in-launch K split for the N = 768 products
+  ktests kt "w4x_split or w4_gated or caption_dx or strided_output or test_gemm_w4x or tile128x192 or splitk_combined or grouped_wgrad or test_gemm_w4 or bias_dropout_residual"
+  for r in 1 2; do for v in 1 0; do GVL_W4X_SPLIT=$v bench qf_s${v}_$r qformer; done; done
+  for v in 1 0; do GVL_W4X_SPLIT=$v bench lin_s${v} linear; GVL_W4X_SPLIT=$v bench cross_s${v} cross; done
+  for M in 8064 4096; do for v in 1 0; do GVL_W4X_SPLIT=$v diag s$v $M narrow epi; done; done
+  ;;
+r5c)  # two-slice split (GVL_W4X_SPLIT=1) A/B; attention row max by lane swaps A/B; Q-Former grad scale
+  ktests kt "w4x_split or caption_dx or test_gemm_w4x or tile128x192 or attention"
+  for v in 1 0 1 0; do GVL_W4X_SPLIT=$v diag s$v 8064 narrow epi; done
+  for r in 1 2; do for v in 1 0; do GVL_W4X_SPLIT=$v bench qf_s${v}_$r qformer; done; done
+  for r in 1 2; do for L in base shfl; do
+    LIB=$LIBDIR/libgvl.so; [ $L = shfl ] && LIB=$LIBDIR/libgvl_shfl.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; head -3 $O/attn_${L}_$r.log
+  done; done
+  GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "qformer" tests/test_gpu_parity_bench.py
+  ;;
+*) echo "unknown session $S"; exit 2 ;;
+esac
