@@ -16,6 +16,7 @@
 // log-sum-exp.  Dropout (Q-Former MHA) is a counter-hash mask on (b,h,q,k), identical in
 // every kernel.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "capi_util.h"
@@ -396,6 +397,12 @@ GVL_DEV short8_t frag_tr_asm(const char* lds, int t, int s, int lane) {
   r.hi = hi;
   return r;
 }
+// lgkmcnt(N) with the fragments threaded through: all but this wave's N newest LDS operations
+// done (LDS operations complete in order, so the fragments read before the N newest are in)
+template <int N>
+GVL_DEV void lds_wait_n(short8_t (&a)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N) : "memory");
+}
 // lgkmcnt(0), with the fragments threaded through so no use is scheduled above the wait
 GVL_DEV void lds_wait4(short8_t (&a)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : : "memory");
@@ -406,6 +413,21 @@ GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
                  "+v"(b[3])
                :
                : "memory");
+}
+
+// Issue the lse and D float4 of one fragment row (ds_read_b128 at a and a + 256) without waiting;
+// lds_wait_pair<N> waits until at most N of this wave's LDS operations are in flight, with the
+// pair threaded through so no use is scheduled above the wait.  Early-clobber: a result must not
+// land on the address register of the second read.
+GVL_DEV void lds_pair(float4_t& l4, float4_t& d4, const float* a) {
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256"
+               : "=&v"(l4), "=&v"(d4)
+               : "v"((uint32_t)reinterpret_cast<uintptr_t>(a))
+               : "memory");
+}
+template <int N>
+GVL_DEV void lds_wait_pair(float4_t& l4, float4_t& d4) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(l4), "+v"(d4) : "n"(N) : "memory");
 }
 
 // G key groups of 16 per wave (64 G keys per block): every Q / dO fragment read from LDS
@@ -496,7 +518,17 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
     wait_tiles(nq > 1 ? 1 : 0);
     gvl_ring::barrier_lds();
   }
-  for (int i = 0; i < nq; ++i) {
+  // query tiles with no mask for any of this wave's keys (all its keys < Tk and, causal, at or
+  // below the tile's first query; the tile inside Tq) run a body without the mask code: with
+  // causal masking only the first (diagonal) tile and a ragged last one need it
+  const int64_t kw_max = kblk0 + wave * 16 * G + 16 * G - 1;  // this wave's last key
+  const bool keys_in = kw_max < p.Tk;
+  auto masked = [&](int i) {
+    const int64_t q0 = (int64_t)(qt_first + i) * KT;
+    return !keys_in || q0 + KT > p.Tq || (p.causal && kw_max > q0);
+  };
+  auto tile = [&](int i, auto mtag) __attribute__((always_inline)) {
+    constexpr bool MASK = decltype(mtag)::value;
     const int qt = qt_first + i, st = i % 3;
     if (i + 2 < nq) issue(qt + 2, (i + 2) % 3);
     const char* qs = smem + st * DK_SLOT;
@@ -526,19 +558,26 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int64_t kg_max = kblk0 + wave * 16 * G + g * 16 + 15;
-      const bool msk = q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0);
+      const bool msk = MASK && (q0 + KT > p.Tq || kg_max >= p.Tk || (p.causal && kg_max > q0));
       const int kq = (int)(key[g] - q0);
       float4_t pd[4];
+      // lse / D of this lane's 4 queries per fragment row n: read by inline asm, because hipcc
+      // cannot tell these bytes apart from the in-flight lse / D DMA of another slot and would
+      // drain vmcnt(0) (the whole two-ahead prefetch) before a plain read; they landed before the
+      // barrier.  Row n + 1's pair is issued before row n is processed, and the counted wait
+      // leaves it in flight (round 4 waited for each pair with lgkmcnt(0): four exposed LDS round
+      // trips per query tile; PMC r5d: waves parked 37 % of their cycles)
+      float4_t lv[2], dv2[2];
+      lds_pair(lv[0], dv2[0], sl + 4 * Gl);
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        // lse / D of this lane's 4 queries: read by inline asm, because hipcc cannot tell these
-        // bytes apart from the in-flight lse / D DMA of another slot and would drain vmcnt(0)
-        // (the whole two-ahead prefetch) before a plain read; they landed before the barrier.
-        float4_t l4, d4;
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(l4), "=&v"(d4)  // early-clobber: l4 must not sit on the address
-                     : "v"((uint32_t)reinterpret_cast<uintptr_t>(sl + 16 * n + 4 * Gl))
-                     : "memory");
+        if (n < 3) {
+          lds_pair(lv[(n + 1) & 1], dv2[(n + 1) & 1], sl + 16 * (n + 1) + 4 * Gl);
+          lds_wait_pair<2>(lv[n & 1], dv2[n & 1]);
+        } else {
+          lds_wait_pair<0>(lv[n & 1], dv2[n & 1]);
+        }
+        const float4_t l4 = lv[n & 1], d4 = dv2[n & 1];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = 16 * n + 4 * Gl + r;
@@ -581,6 +620,10 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
     }
     if (i + 1 < nq) wait_tiles(i + 2 < nq ? 1 : 0);
     gvl_ring::barrier_lds();  // slot st is refilled by iteration i+1's issue
+    };
+  for (int i = 0; i < nq; ++i) {
+    if (masked(i)) tile(i, std::true_type{});
+    else tile(i, std::false_type{});
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -695,7 +738,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gvl_ring::barrier_lds();
   }
-  for (int kt = 0; kt < nkt; ++kt) {
+  // key tiles with no mask for any of this wave's query groups run a body without the mask
+  // code (as attn_fwd_dma_kernel)
+  const int64_t qw0 = qblk0 + wave * 16 * G;
+  int nfull = (int)(p.Tk / KT);
+  if (p.causal) nfull = (int)((qw0 + 1) / KT) < nfull ? (int)((qw0 + 1) / KT) : nfull;
+  nfull = nfull < nkt ? nfull : nkt;
+  auto tile = [&](int kt, auto mtag) __attribute__((always_inline)) {
+    constexpr bool MASK = decltype(mtag)::value;
     if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
     const char* ks = smem + (kt % 3) * SLOT;
     const char* vs = ks + KT * D * 2;
@@ -723,7 +773,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
-      const bool msk = k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0);
+      const bool msk = MASK && (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0));
       const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
 #pragma unroll
       for (int n = 0; n < 4; ++n)
@@ -740,12 +790,17 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
       sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
       sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
     }
+    // K^T fragments of both k-halves issued before the first half's MFMAs (+16 VGPRs; the
+    // kernel is at 2 waves per SIMD either way)
+    short8_t kta[2][4];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kta[s2][t] = frag_tr_asm(ks, t, s2, lane);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      short8_t kt4[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) kt4[t] = frag_tr_asm(ks, t, s2, lane);
-      lds_wait4(kt4);
+      short8_t (&kt4)[4] = kta[s2];
+      if (s2 == 0) lds_wait_n<8>(kt4); else lds_wait4(kt4);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -756,7 +811,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     gvl_ring::barrier_lds();
-  }
+    };
+  int kt = 0;
+  for (; kt < nfull; ++kt) tile(kt, std::false_type{});
+  for (; kt < nkt; ++kt) tile(kt, std::true_type{});
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (!qok[g]) continue;
@@ -848,7 +906,16 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gvl_ring::barrier_lds();
   }
-  for (int kt = 0; kt < nkt; ++kt) {
+  // Key tiles that need no mask for any of this wave's query groups (inside Tk, and at or below
+  // the wave's first query) run a body compiled without the mask code: hipcc hoisted the
+  // boundary compares of the masked branch above it, 16 v_cmp per group on EVERY tile (PMC r5d:
+  // ~230 VALU instructions per wave and tile, the softmax's VALU half the SIMD's cycles)
+  const int64_t qw0 = qblk0 + wave * 16 * G;
+  int nfull = (int)(p.Tk / KT);
+  if (p.causal) nfull = (int)((qw0 + 1) / KT) < nfull ? (int)((qw0 + 1) / KT) : nfull;
+  nfull = nfull < nkt ? nfull : nkt;
+  auto tile = [&](int kt, auto mtag) __attribute__((always_inline)) {
+    constexpr bool MASK = decltype(mtag)::value;
     if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
     const char* ks = smem + (kt % 3) * SLOT;
     const char* vs = ks + KT * D * 2;
@@ -869,7 +936,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
-      if (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0)) {
+      if (MASK && (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0))) {
         const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
 #pragma unroll
         for (int n = 0; n < 4; ++n)
@@ -906,12 +973,17 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
       pf[g][0] = pack_frag(sc[g][0], sc[g][1]);
       pf[g][1] = pack_frag(sc[g][2], sc[g][3]);
     }
+    // V fragments of both k-halves issued before the first half's MFMAs (the second half's
+    // LDS latency hides behind them; +16 VGPRs, still 3 waves per SIMD)
+    short8_t vfa[2][4];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vfa[s2][t] = frag_tr_asm(vs, t, s2, lane);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      short8_t vf[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) vf[t] = frag_tr_asm(vs, t, s2, lane);
-      lds_wait4(vf);
+      short8_t (&vf)[4] = vfa[s2];
+      if (s2 == 0) lds_wait_n<8>(vf); else lds_wait4(vf);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -924,7 +996,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     gvl_ring::barrier_lds();
-  }
+    };
+  int kt = 0;
+  for (; kt < nfull; ++kt) tile(kt, std::false_type{});
+  for (; kt < nkt; ++kt) tile(kt, std::true_type{});
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float lt = o[g][4][0];

@@ -227,11 +227,10 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
 
 namespace gvl {
 bool pp3_combine_forced() { return env().impl >= 3 && env().cfg == 13; }
-bool w4x_split_forced() { return env().impl >= 3 && env().cfg == 14; }
 }  // namespace gvl
 
 extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
-  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 14, "gvl_gemm_tune: bad arguments");
+  GVL_REQUIRE(impl >= 0 && impl <= 3 && cfg >= -1 && cfg <= 13, "gvl_gemm_tune: bad arguments");
   env().impl = impl;
   env().cfg = cfg;
   return 0;
@@ -240,15 +239,12 @@ extern "C" int gvl_gemm_tune(int32_t impl, int32_t cfg) {
 extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t len) {
   GVL_REQUIRE(d && buf && len > 0, "gvl_gemm_kernel_name: bad arguments");
   const char* tf[2] = {"false", "true"};
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12 || env().cfg == 14)) {
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12)) {
     GemmP q;
     fill_params(d, q);
     if (gvl::gemm_w4x_plan(q, d->a_mn, d->b_mn, env().cfg == 12)) {
-      if (q.splits > 1)
-        snprintf(buf, len, "gemm_w4xs_kernel<%s, %d>", tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
-      else
-        snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d, false>", q.bm, d->a_mn ? q.bn : 192,
-                 tf[d->a_mn != 0], tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
+      snprintf(buf, len, "gemm_w4x_kernel<%d, %d, %s, %s, %d, false>", q.bm, d->a_mn ? q.bn : 192,
+               tf[d->a_mn != 0], tf[d->b_mn != 0], gvl::gemm_epi_kind(q));
       return 0;
     }
   }
@@ -310,7 +306,7 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
   GemmP p;
   fill_params(d, p);
   hipStream_t s = gvl::as_stream(stream);
-  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12 || env().cfg == 14) &&
+  if (env().impl >= 3 && (env().cfg < 0 || env().cfg == 12) &&
       gvl::gemm_w4x_try(p, d->a_mn, d->b_mn, env().cfg == 12, s)) {  // AGPR four-wave kernel
     GVL_LAUNCH_CHECK("gvl_gemm(w4x)");
     return 0;

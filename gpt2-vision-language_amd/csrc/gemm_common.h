@@ -523,7 +523,6 @@ int gemm_epi_kind(const GemmP& p);  // EPI_* for the persistent kernels (gemm_pl
 bool gemm_pp3_plan(GemmP& p, bool force, int gran = 32);  // gran: K-step depth
 bool gemm_pp3_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 bool pp3_combine_forced();  // gemm.hip: gvl_gemm_tune(3, 13) (the persistent kernel's combine, tests)
-bool w4x_split_forced();    // gemm.hip: gvl_gemm_tune(3, 14) (the AGPR kernel's K split, tests)
 int gemm_pp3_launch(const GemmP& p, int a_mn, int b_mn, hipStream_t s);  // planned p
 int gemm_pp3_launch_ff(const GemmP& p, hipStream_t s);  // gemm_pp3_{ff,ft,tf,tt}.hip
 int gemm_pp3_launch_ft(const GemmP& p, hipStream_t s);

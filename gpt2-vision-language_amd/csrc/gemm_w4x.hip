@@ -68,90 +68,6 @@ GVL_DEV void w4x_piece(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, soff, 0, 0);
 }
 
-// In-launch K split (SPL instances; w4x_split_plan): the S work items of one output tile run
-// K-slices [s kper, (s + 1) kper) on S CUs and meet inside the launch, arrival first.  Per
-// (tile, wave) two agent-scope counters: `arrive` orders the S waves that own the same 128 x 96
-// block; the first S - 1 publish their fp32 partial (write-through sc1 16-B stores into slab s of
-// the workspace, s_waitcnt vmcnt(0)) and bump `published`; the last one polls `published` (sc1
-// loads, bounded) — every wave it waits for has already arrived, i.e. is running and has nothing
-// left to wait on, so the poll always ends — then resets both counters, loads the S - 1 partials
-// with sc1 loads and sums all S slices in split order (so the result does not depend on which
-// slice arrived last), and runs the epilogue.  Only the last arriver writes C; nobody writes a
-// partial that nobody reads.  Memory protocol: MI355X_MICROARCH.md, Valid forms, row 1 (one
-// lane per storing wave signals for that wave's own sc1 stores after its vmcnt(0) wait; the
-// consumer wave loads only those bytes, by sc1 loads, after its poll has matched).
-GVL_DEV uint32_t* w4x_ticket(const GemmP& p, int tile, int wave) { return p.tickets + ((int64_t)tile * 4 + wave) * 2; }
-
-// returns true in the wave that arrived last (it then owns the epilogue)
-template <int FM, int FN>
-GVL_DEV bool w4x_split_arrive(const GemmP& p, const float4_t (&acc)[FM][FN], int split, int tile,
-                              int wave, int64_t mw0, int64_t nw0, int lane) {
-  typedef __attribute__((address_space(1))) uint32_t gu32;
-  gu32* const arr = (gu32*)w4x_ticket(p, tile, wave);
-  gu32* const pub = arr + 1;
-  uint32_t got = 0;
-  if (lane == 0) got = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  got = __builtin_amdgcn_readfirstlane(got);
-  if ((int)got + 1 < p.splits) {  // not last: publish this slice's partial
-    const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws, p.ws_bytes);
-    const int voff = (int)(((int64_t)(lane & 15) * p.N + 4 * (lane >> 4)) * 4);
-    const int64_t base = (int64_t)split * p.M * p.N + mw0 * p.N + nw0;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const bool mok = mw0 + i * 16 + (lane & 15) < p.M;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int soff = __builtin_amdgcn_readfirstlane((int)((base + (int64_t)i * 16 * p.N + j * 16) * 4));
-        if (mok && nw0 + j * 16 < p.N)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), rw, voff, soff, 16);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(pub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-  }
-  if (lane == 0) {
-    // bounded poll (~1 s at 2 GHz): the waves polled for are running, so it ends long before;
-    // the bound only keeps a broken launch from hanging the device
-    for (int it = 0; it < (1 << 22); ++it) {
-      if ((int)__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= p.splits - 1) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  (void)__builtin_amdgcn_readfirstlane(got);  // the wave continues past lane 0's poll together
-  return true;
-}
-
-// last arriver: acc += the other slice's partial (two slices: fp32 addition commutes, so the
-// result does not depend on which slice arrived last), by sc1 loads in two batches of half the
-// fragment rows, all of a batch in flight at once (a round trip per fragment row measured
-// ~2x slower than the whole K-loop gain); rows past M read inside the workspace (or past its
-// end: zero) and are never stored
-template <int FM, int FN>
-GVL_DEV void w4x_split_gather(const GemmP& p, float4_t (&acc)[FM][FN], int split, int64_t mw0,
-                              int64_t nw0, int lane) {
-  const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(p.ws, p.ws_bytes);
-  const int voff = (int)(((int64_t)(lane & 15) * p.N + 4 * (lane >> 4)) * 4);
-  const int64_t base = (int64_t)(1 - split) * p.M * p.N + mw0 * p.N + nw0;
-  constexpr int H = FM / 2;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    u32x4_t t[H][FN];
-#pragma unroll
-    for (int i = 0; i < H; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        t[i][j] = __builtin_amdgcn_raw_buffer_load_b128(
-            rw, voff, __builtin_amdgcn_readfirstlane((int)((base + (int64_t)(h * H + i) * 16 * p.N + j * 16) * 4)), 16);
-#pragma unroll
-    for (int i = 0; i < H; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[h * H + i][j] += __builtin_bit_cast(float4_t, t[i][j]);
-  }
-}
-
 // B fragment of an MN-contiguous 192-wide slab (the Step192<true> image: columns 0-127 as
 // [32][128] 256-B rows with the fT swizzle, 128-191 as [32][64] 128-B rows at +8 KiB with f2)
 // by inline asm: hipcc treats the ds_read_b64_tr_b16 builtin as possibly aliasing any LDS-DMA
@@ -243,10 +159,7 @@ struct XSlabB<256, MN> {
 // waves of 128 x 128 (8 x 8 fragments = all 256 AGPRs, 0.25 reads per MFMA).
 // GR: a grouped launch (gvl_gemm_grouped): the problems differ in M, N, K and strides
 // (GemmP::Mb.. / gtile), read per tile.
-// SPL: the in-launch K split (w4x_split_arrive): S = p.splits work items per tile; those
-// instances are the separately named gemm_w4xs_kernel (below), so the whole-K instances keep
-// their names in the profiles.
-template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR, bool SPL>
+template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR>
 GVL_DEV void gemm_w4x_body(const GemmP& p) {
   constexpr int NS = x_ns<BM>(), FM = BM / 32, FN = BN / 32;
   using SA = Step<BM, AMN, 4>;                // 16 / 8 pieces: 4 / 2 per wave
@@ -260,7 +173,7 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int arow = (wave >> 1) * (BM / 2), bcol = (wave & 1) * (BN / 2);
-  const int per_batch = p.tiles_m * p.tiles_n * (SPL ? p.splits : 1);
+  const int per_batch = p.tiles_m * p.tiles_n;
   const int total = GR ? p.gtile[p.batch] : per_batch * p.batch;
   const int G = gridDim.x;
   __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A, (AMN ? p.K : p.M) * p.lda * 2);
@@ -302,12 +215,11 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
       bi = work / per_batch;
       local = work - bi * per_batch;
     }
-    const int nks = (int)((SPL ? p.kper : K_) / KS);
+    const int nks = (int)(K_ / KS);
     const int64_t a_rows = AMN ? K_ : M_, b_rows = BMN ? K_ : N_;
     const int sa_step = SA::step_bytes(lda_), sb_step = SB::step_bytes(ldb_);
     int split, tm, tn;
-    gemm_tile_of(local, SPL ? p.splits : 1, tiles_m, tiles_n, p.group, split, tm, tn);
-    const int64_t k0 = SPL ? (int64_t)split * p.kper : 0;  // this item's K-slice
+    gemm_tile_of(local, 1, tiles_m, tiles_n, p.group, split, tm, tn);
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
     // per-problem operands: a batched launch of several problems, or a grouped one of any count
     // (a grouped launch of ONE problem still carries its bias sum in Db[0])
@@ -320,8 +232,8 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
     }
     bool do_db = false;
     if constexpr (DB) do_db = multi && n0 == 0 && p.Db[bi] != nullptr;
-    SA::base_offsets(lda_, m0, k0, wave, lane, offa);
-    SB::base_offsets(ldb_, n0, k0, wave, lane, offb);
+    SA::base_offsets(lda_, m0, 0, wave, lane, offa);
+    SB::base_offsets(ldb_, n0, 0, wave, lane, offb);
     // the first half of the epilogue operand (residual) is fetched two K-steps before the tile
     // ends (at the epilogue its latency is exposed: one tile per CU on the routed shapes); the
     // whole of it would spill
@@ -381,7 +293,7 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
       wait_vm_steps<PER, NS - 3>(r_ < 0 ? 0 : (r_ < NS - 3 ? r_ : NS - 3));                    \
     }                                                                                          \
     __builtin_amdgcn_s_barrier();                                                              \
-    if (!(FULL) && !BMN && !SPL && EpiKind<EPI>::AUX && (c) == aux_at) /* BMN, SPL: spills */   \
+    if (!(FULL) && !BMN && EpiKind<EPI>::AUX && (c) == aux_at)  /* BMN: it would spill */        \
       pre.load_aux(p, m0 + arow, n0 + bcol, lane, 0, res), pre.pre0 = true;                   \
     const bool nx_ = FULL || (c) + 1 < nks, dm_ = FULL || (c) + NS - 1 < nks;                  \
     const char* sl_ = smem + (((c) + 1) % NS) * SLOT;                                          \
@@ -434,17 +346,6 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
     w4x_fence(acc);
     // every wave is past its last fragment read of this tile before anyone's next prologue DMA
     __builtin_amdgcn_s_barrier();
-    if constexpr (SPL) {
-      const int tile = local / p.splits;
-      if (!w4x_split_arrive<FM, FN>(p, acc, split, tile, wave, m0 + arow, n0 + bcol, lane)) continue;
-      // the last arriver fetches the first half of the epilogue operand (residual) before the
-      // partial, so the two latencies overlap
-      if constexpr (EpiKind<EPI>::AUX && !BMN) {
-        pre.load_aux(p, m0 + arow, n0 + bcol, lane, 0, res);
-        pre.pre0 = true;
-      }
-      w4x_split_gather<FM, FN>(p, acc, split, m0 + arow, n0 + bcol, lane);
-    }
     if constexpr (GR) {  // this problem's sizes for the epilogue (only the scalars used survive)
       GemmP q = p;
       q.M = M_, q.N = N_, q.ldc = ldc_, q.ldr = ldc_;
@@ -465,36 +366,25 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
   }
 }
 
+// (a device body under a thin __global__: target builtins and "a"-constrained asm in a
+// __global__ body make clang drop the kernel's host stub)
 template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
-  gemm_w4x_body<BM, BN, AMN, BMN, EPI, GR, false>(p);
-}
-template <bool BMN, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4xs_kernel(GemmP p) {
-  gemm_w4x_body<256, 192, false, BMN, EPI, false, true>(p);
+  gemm_w4x_body<BM, BN, AMN, BMN, EPI, GR>(p);
 }
 
-template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false, bool SPL = false>
+template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false>
 void launch_w4x(const GemmP& p, hipStream_t s) {
+  auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI, GR>;
   static bool attr_set = false;
-  constexpr int lds = x_ns<BM>() * (BM + BN) * KS * 2;
-  const int total = GR ? p.gtile[p.batch] : p.tiles_m * p.tiles_n * p.batch * (SPL ? p.splits : 1);
-  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
-  if constexpr (SPL) {
-    auto kern = gemm_w4xs_kernel<BMN, EPI>;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
-  } else {
-    auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI, GR>;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
   }
+  const int total = GR ? p.gtile[p.batch] : p.tiles_m * p.tiles_n * p.batch;
+  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
+  constexpr int lds = x_ns<BM>() * (BM + BN) * KS * 2;
+  gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
 }
 
 template <int BM, bool BMN>
@@ -505,21 +395,6 @@ bool launch_w4x_epi(const GemmP& p, hipStream_t s) {
     default: return false;
   }
 }
-// the split instances: plain (dX, b_mn = 1; forward plain, b_mn = 0) and bias + residual (forward)
-template <bool BMN>
-bool launch_w4x_split(const GemmP& p, hipStream_t s) {
-  switch (gvl::gemm_epi_kind(p)) {
-    case EPI_PLAIN: launch_w4x<256, 192, false, BMN, EPI_PLAIN, false, true>(p, s); return true;
-    case EPI_BIAS_RES:
-      if constexpr (!BMN) {
-        launch_w4x<256, 192, false, false, EPI_BIAS_RES, false, true>(p, s);
-        return true;
-      }
-      return false;
-    default: return false;
-  }
-}
-
 }  // namespace
 
 namespace gvl {
@@ -540,46 +415,13 @@ int w4x_mode() {
 // tiling fills the chip in whole rounds (M = 16384, N = 768: 256 tiles).
 bool w4x_dw_plan(GemmP& p);
 
-// In-launch K split for N = 768 outputs whose 256 x 192 tiles fill half the chip (the caption
-// decoders' 8064 / 8192 rows: 128 tiles, S = 2): S work items per tile, each a K-slice of at least 6 steps, combined in the launch
-// (w4x_split_arrive).  Against one 192 x 128 tile per CU (gemm_w4d_kernel) a CU streams
-// (256 + 192) instead of (192 + 128) operand rows per 256 x 192 instead of 192 x 128 outputs:
-// 30 % fewer bytes per MFMA from L2, which is what the narrow GEMMs run out of (DESIGN §3,
-// round 5).  Needs the caller's workspace (S fp32 slabs of M x N) and tickets (8 per tile).
-// Off by default (GVL_W4X_SPLIT=1 or gvl_gemm_tune(3, 14) turn it on; see DESIGN round 5 for the
-// measurement); GVL_W4X_SPLIT_KMIN=k takes only K >= k.
-static bool w4x_split_plan(GemmP& p, int epi, int b_mn) {
-  static const int on_env = [] {
-    const char* e = getenv("GVL_W4X_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  const int on = on_env || w4x_split_forced();  // gvl_gemm_tune(3, 14): tests
-  static const int64_t kmin = [] {
-    const char* e = getenv("GVL_W4X_SPLIT_KMIN");
-    return e ? atol(e) : 0L;
-  }();
-  if (on == 0 || w4x_mode() == 0 || p.N != 768 || p.K < kmin || !p.ws || !p.tickets) return false;
-  if (epi != EPI_PLAIN && !(epi == EPI_BIAS_RES && !b_mn)) return false;
-  const int64_t cus = num_cus(), tiles = ((p.M + 255) / 256) * 4;
-  int S = 1;
-  while (tiles * S * 2 <= cus && S < 2) S *= 2;  // two slices only (w4x_split_gather)
-  if (S == 1 || tiles * S * 10 < cus * 9 || p.K % (KS * S) != 0 || p.K / S < 6 * KS) return false;
-  if (tiles * 8 > p.nticket || (int64_t)S * p.M * p.N * 4 > p.ws_bytes) return false;
-  p.bm = 256;
-  p.tiles_m = (int)((p.M + 255) / 256);
-  p.tiles_n = 4;
-  p.splits = S;
-  p.kper = p.K / S;
-  return true;
-}
-
 bool gemm_w4x_plan(GemmP& p, int a_mn, int b_mn, bool force) {
   const int epi = gemm_epi_kind(p);
   if (a_mn) return p.batch == 1 && w4x_dw_plan(p) && p.K >= 4096;  // the lm_head's dW (b_mn)
   if ( p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.N % 8 != 0 || p.ldc % 8 != 0 ||
       p.lda % 8 != 0 || p.ldb % 8 != 0 || (epi != EPI_PLAIN && epi != EPI_BIAS_RES))
     return false;
-  if (w4x_split_plan(p, epi, b_mn)) return true;
+  (void)b_mn;
   // 256-row tiles where they (nearly) fill the chip, else 128-row tiles
   const int64_t cus = num_cus(), tn = (p.N + 192 - 1) / 192;
   p.bm = ((p.M + 255) / 256) * tn * 10 >= cus * 9 ? 256 : 128;
@@ -605,7 +447,6 @@ bool gemm_w4x_try(const GemmP& p0, int a_mn, int b_mn, bool force, hipStream_t s
   GemmP p = p0;
   if (!gemm_w4x_plan(p, a_mn, b_mn, force)) return false;
   if (a_mn) return b_mn && gemm_w4x_dw_try(p0, s);
-  if (p.splits > 1) return b_mn ? launch_w4x_split<true>(p, s) : launch_w4x_split<false>(p, s);
   if (p.bm == 256) return b_mn ? launch_w4x_epi<256, true>(p, s) : launch_w4x_epi<256, false>(p, s);
   return b_mn ? launch_w4x_epi<128, true>(p, s) : launch_w4x_epi<128, false>(p, s);
 }

@@ -99,9 +99,8 @@ def _gemm_workspace(device):
 
 _TK = {}
 GEMM_TICKETS = 1 << 16
-# Arrival tickets (gvl.h ABI v5) go with every gvl_gemm call: the AGPR four-wave kernel's
-# in-launch K split of the caption decoders' N = 768 products uses them (gemm_w4x.hip); the
-# persistent kernel's own two-way combine stays off unless GVL_PP3_COMBINE=1 (checked in C).
+# Arrival tickets (gvl.h ABI v5) go with every gvl_gemm call; the persistent kernel's in-launch
+# two-way combine that uses them stays off unless GVL_PP3_COMBINE=1 (checked in C, gemm_plan.hip).
 # Batched weight gradients may use it (gvl_gemm_batched decides; GVL_BATCHED_SPLIT=0: never).
 BATCHED_SPLIT = os.environ.get("GVL_BATCHED_SPLIT", "1") != "0"
 

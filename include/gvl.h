@@ -125,10 +125,8 @@ int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
  * them (and without the AGPR four-wave kernel), 12 (ABI v8, round 4) the AGPR four-wave kernel
  * (gemm_w4x.hip: 256 x 192 / 128 x 192 tiles, K-contiguous A, plain or bias + residual) where
  * it applies; 13 (ABI v10) = cfg 11 with the persistent kernel's in-launch two-way combine
- * enabled for single GEMMs (tests; otherwise only with env GVL_PP3_COMBINE=1, since the caller's
- * tickets now also serve the AGPR kernel's split); 14 (ABI v10) = default routing with the AGPR
- * kernel's in-launch K split of the caption decoders' N = 768 products (gemm_w4xs_kernel; off by
- * default, env GVL_W4X_SPLIT=1); other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase
+ * enabled for single GEMMs (tests; otherwise only with env GVL_PP3_COMBINE=1, since the
+ * callers' tickets are passed to every gvl_gemm by gvl.kernels); other cfg values route as -1.  impl 4 (the removed 64-deep quadrant-phase
  * kernel) is rejected. */
 int gvl_gemm_tune(int32_t impl, int32_t cfg);
 /* Name of the kernel template instance gvl_gemm would launch for d (profiling: lets a

@@ -174,7 +174,7 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
-@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 4096, 0, 0),
+@pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 3072, 0, 0),
                                                (4096, 768, 3072, 0, 1)])
 def test_gemm_caption_dx_on_own_kernels(cuda, M, N, K, a_mn, b_mn):
     """The plain N = 768 products that round 4 handed to hipBLASLt (the caption decoder's and the
@@ -257,56 +257,6 @@ def test_gemm_w4x(cuda, b_mn, epi, M, N, K):
         assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi).startswith("gemm_w4x_kernel")
     assert rel_err(out.float().cpu().numpy(), ref.numpy()) < 8e-3
     assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
-
-
-@pytest.mark.parametrize("M,N,K,b_mn,epi,S", [
-    (8064, 768, 3072, 1, "plain", 2), (8064, 768, 3072, 0, "bias_res", 2),
-    (8064, 768, 768, 0, "bias_res", 2), (8064, 768, 2304, 1, "plain", 2),
-    (8192, 768, 3072, 1, "plain", 2), (8000, 768, 384, 0, "plain", 2)])
-def test_gemm_w4x_split(cuda, M, N, K, b_mn, epi, S):
-    """The AGPR four-wave kernel's in-launch K split (gemm_w4xs_kernel, round 5): the caption
-    decoders' and the Q-Former's N = 768 products as S K-slices per 256 x 192 tile meeting in
-    the launch.  Chosen by default at these shapes (checked by name); vs the fp32 product; the
-    slices are summed in split order, so two runs are bit-identical; the arrival counters are
-    left zero; replayed from a captured hipGraph; ragged M (the last tile row part-empty)."""
-    from gvl import _lib
-    K_ = _k()
-    torch.manual_seed(M + N + K + b_mn + S)
-    a = torch.randn(M, K).to(BF)
-    b = (torch.randn(K, N) * 0.05).to(BF)
-    A = a.to(cuda)
-    B = (b if b_mn else b.t().contiguous()).to(cuda)
-    _lib.lib().gvl_gemm_tune(3, 14)  # the split is off by default (DESIGN, round 5)
-    try:
-        _run_w4x_split(K_, A, B, a, b, M, N, K, b_mn, epi, cuda)
-    finally:
-        _lib.lib().gvl_gemm_tune(3, -1)
-
-
-def _run_w4x_split(K_, A, B, a, b, M, N, K, b_mn, epi, cuda):
-    assert _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi) == f"gemm_w4xs_kernel<{'true' if b_mn else 'false'}, " \
-        f"{0 if epi == 'plain' else 2}>"
-    h = a.float() @ b.float()
-    kw, ref = {}, h
-    if epi == "bias_res":
-        bias, res = torch.randn(N).to(BF), torch.randn(M, N).to(BF)
-        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
-    big = torch.full((M + 3, N + 8), 7.0, dtype=BF, device=cuda)
-    out = big[:M, :N]
-    outs = []
-    for _ in range(2):
-        K_.gemm(A, B, b_mn=bool(b_mn), out=out, **kw)
-        outs.append(out.clone())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        K_.gemm(A, B, b_mn=bool(b_mn), out=out, **kw)
-    out.fill_(0.0)
-    g.replay()
-    torch.cuda.synchronize()
-    assert rel_err(outs[0].float().cpu().numpy(), ref.numpy()) < 8e-3
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
-    assert torch.all(big[:, N:] == 7.0) and torch.all(big[M:, :] == 7.0)
-    assert int(K_._gemm_tickets(A.device).abs().sum()) == 0
 
 
 @pytest.mark.parametrize("epi", ["plain", "bias", "bias_act_d", "bias_act_erf_d"])
@@ -519,9 +469,7 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
     A = (a.t().contiguous() if a_mn else a).to(cuda)
     B = (b if b_mn else b.t().contiguous()).to(cuda)
     name = _kernel_name(A, B, a_mn, b_mn, M, N, K, epi=epi)
-    if not a_mn and os.environ.get("GVL_W4X_SPLIT") == "1" and _w4xs_name(M, N, K, b_mn, epi):
-        assert name == _w4xs_name(M, N, K, b_mn, epi), name  # (the AGPR kernel's K split, A/B)
-    elif not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
+    if not a_mn and K % 192 == 0:  # K-contiguous A: a four-wave 192x128 kernel takes it
         assert name.startswith(_w4_name(M, K, epi)), name
     elif a_mn and K >= 3072:  # with gvl.kernels' workspace the planner splits K: 128x128 ring
         assert name.startswith("gemm_ring_kernel") or name.endswith(", 192, 128>"), name
@@ -558,22 +506,6 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
 
 # epilogues gemm_w4d_kernel is instantiated for (gemm_w4d.h epi_supported)
 W4D_EPIS = ("plain", "bias", "bias_res", "res_inplace", "drop_res")
-
-
-def _w4xs_name(M, N, K, b_mn, epi):
-    """The AGPR kernel's in-launch K split (gemm_w4x.hip w4x_split_plan) for this
-    K-contiguous-A shape when the split is on (GVL_W4X_SPLIT=1 / gvl_gemm_tune(3, 14)), else None."""
-    if N != 768:
-        return None
-    if not (epi == "plain" or (epi == "bias_res" and not b_mn)):
-        return None
-    tiles = (M + 255) // 256 * 4
-    S = 1
-    while tiles * S * 2 <= 256 and S < 2:
-        S *= 2
-    if S == 1 or tiles * S * 10 < 256 * 9 or K % (32 * S) or K // S < 192:
-        return None
-    return f"gemm_w4xs_kernel<{'true' if b_mn else 'false'}, {0 if epi == 'plain' else 2}>"
 
 
 def _w4_name(M, K, epi):

@@ -58,5 +58,28 @@ r5c)  # two-slice split (GVL_W4X_SPLIT=1) A/B; attention row max by lane swaps A
   done; done
   GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "qformer" tests/test_gpu_parity_bench.py
   ;;
+r5d)  # attention row max by lane swaps vs ds_bpermute (libgvl_shfl.so) A/B; Q-Former grad scale
+  ktests kt "attention or attn or caption_dx or test_gemm_w4x or tile128x192"
+  for r in 1 2; do for L in base shfl; do
+    LIB=$LIBDIR/libgvl.so; [ $L = shfl ] && LIB=$LIBDIR/libgvl_shfl.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep "B=" $O/attn_${L}_$r.log | head -3
+  done; done
+  for r in 1 2; do for L in base shfl; do
+    LIB=$LIBDIR/libgvl.so; [ $L = shfl ] && LIB=$LIBDIR/libgvl_shfl.so
+    GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "qformer" tests/test_gpu_parity_bench.py
+  bash tools/pmc_attn.sh $S; fatal $? pmc_attn
+  ;;
+r5e)  # attention LDS reads software-pipelined (fwd V, dQ K^T, dK/dV lse/D) vs r5d's (libgvl_att0.so)
+  ktests kt "attention or attn" tests/test_gpu_kernels.py
+  for r in 1 2 3; do for L in base att0; do
+    LIB=$LIBDIR/libgvl.so; [ $L = att0 ] && LIB=$LIBDIR/libgvl_att0.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep "B=" $O/attn_${L}_$r.log | head -2
+  done; done
+  GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "linear or cross or lm" tests/test_gpu_parity_bench.py
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
