@@ -45,9 +45,18 @@ def compare(kind, build, run):
     lbf, gbf = grads(mbf, run, True)
     err = {n: float((gbf[n] - g32[n]).norm() / g32[n].norm().clamp_min(1e-30)) for n in g32}
     worst = max(err.items(), key=lambda kv: kv[1])
+    # signed projection error per tensor and the global norm (round 5: a systematic gradient
+    # scale error shows in these, not in the rel-L2 noise)
+    scale = {n: float((gbf[n] * g32[n]).sum() / (g32[n] * g32[n]).sum().clamp_min(1e-300) - 1.0) for n in g32}
+    n32 = float(torch.sqrt(sum((g * g).sum() for g in g32.values())))
+    nbf = float(torch.sqrt(sum((g * g).sum() for g in gbf.values())))
     rec = dict(loss_fp32=l32, loss_bf16=lbf, loss_rel=abs(lbf - l32) / abs(l32),
                worst=worst, median=float(np.median(list(err.values()))), grad_rel_l2=err,
+               grad_norm_fp32=n32, grad_norm_bf16=nbf, grad_norm_rel=(nbf - n32) / n32,
+               scale_err=scale, scale_err_median=float(np.median(list(scale.values()))),
                seconds=round(time.time() - t0, 1))
+    print(kind, f"grad norm rel {rec['grad_norm_rel']:+.2e}, scale err median "
+          f"{rec['scale_err_median']:+.2e}", flush=True)
     print(kind, f"loss rel {rec['loss_rel']:.2e} worst {worst[1]:.3e} ({worst[0]}) median "
           f"{rec['median']:.3e} in {rec['seconds']}s", flush=True)
     return rec

@@ -81,5 +81,23 @@ r5e)  # attention LDS reads software-pipelined (fwd V, dQ K^T, dK/dV lse/D) vs r
   done; done
   GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "linear or cross or lm" tests/test_gpu_parity_bench.py
   ;;
+r5f)  # Q-Former gradient probes vs the reference
+  GVL_MARGINS_DIR=$O/parity_margins ktests probe "grad_probe" tests/test_gpu_parity_bench.py
+  python -c "import json;print(json.dumps(json.load(open('$O/parity_margins/qformer_grad_probe.json')),indent=1))"
+  ;;
+r5g|r5fin|r5fin2|r5fin3)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
+  suite
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],[(k,d[k]['value']) for k in d if k.startswith('caption')])"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  for w in cross linear; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o $w -- \
+      python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_$w.json 2> $O/prof_$w.err; fatal $? prof_$w
+  done
+  for w in qf lm cross linear; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -12 $O/${w}_table.txt; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
