@@ -433,12 +433,20 @@ bool gemm_w4x_plan(GemmP& p, int a_mn, int b_mn, bool force) {
   if (w4x_mode() == 0) return false;
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
   if (p.bm == 256) return p.N == 768 && tiles >= cus && tiles % cus == 0;
-  // 128-row tiles: the caption decoder's 8064 x 768 outputs (252 tiles, one round); A/B
-  static const bool rows128 = [] {
+  // 128-row tiles (GVL_W4X_128: 0 never, 1 wherever they fill one round, 2 = default: only where
+  // the direct-A kernel's 192 x 128 tiles overflow one round).  At the Q-Former / cross decoders'
+  // 8064 rows the direct-A kernel fills one round (252 tiles) and is faster in the step (round 4
+  // r4r and round 5 r5a: 15.45k vs 15.63k images/s with 128-row AGPR tiles); the linear caption
+  // decoder's 8192 rows are 258 of its tiles (a second round for 2 tiles), which sent those
+  // GEMMs to the 128 x 128 ring kernel (59-71 us, 30 % of the linear step in r5g) — here they
+  // are exactly 256 tiles of 128 x 192
+  static const int rows128 = [] {
     const char* e = getenv("GVL_W4X_128");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : 2;
   }();
-  return rows128 && p.N == 768 && tiles * 10 >= cus * 9 && tiles <= cus;
+  const int64_t t_direct = ((p.M + 191) / 192) * ((p.N + 127) / 128);
+  const bool want = rows128 == 1 || (rows128 == 2 && t_direct > cus);
+  return want && p.N == 768 && tiles * 10 >= cus * 9 && tiles <= cus;
 }
 
 bool gemm_w4x_dw_try(const GemmP& p0, hipStream_t s);

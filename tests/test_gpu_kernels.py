@@ -174,6 +174,32 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     return buf.value.decode()
 
 
+@pytest.mark.parametrize("K,b_mn,epi", [(3072, 1, "plain"), (2304, 1, "plain"), (768, 1, "plain"),
+                                         (3072, 0, "bias_res"), (768, 0, "bias_res")])
+def test_gemm_linear_decoder_rows(cuda, K, b_mn, epi):
+    """The linear caption decoder's 8192-row N = 768 GEMMs: 258 of the direct-A kernel's 192 x 128
+    tiles (one round and 2 tiles), so the default routing takes the AGPR kernel's 128 x 192 tiles
+    (exactly 256); vs the fp32 product (round 5; before: the 128 x 128 ring kernel)."""
+    K_ = _k()
+    M, N = 8192, 768
+    torch.manual_seed(K + b_mn)
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(K, N) * 0.05).to(BF)
+    A = a.to(cuda)
+    B = (b if b_mn else b.t().contiguous()).to(cuda)
+    name = _kernel_name(A, B, 0, b_mn, M, N, K, epi=epi)
+    if os.environ.get("GVL_W4X_128", "2") != "0":
+        assert name.startswith("gemm_w4x_kernel<128, 192"), name
+    h = a.float() @ b.float()
+    kw, ref = {}, h
+    if epi == "bias_res":
+        bias, res = torch.randn(N).to(BF), torch.randn(M, N).to(BF)
+        kw, ref = dict(bias=bias.to(cuda), residual=res.to(cuda)), h + bias.float() + res.float()
+    y = K_.gemm(A, B, b_mn=bool(b_mn), **kw)
+    torch.cuda.synchronize()
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+
+
 @pytest.mark.parametrize("M,N,K,a_mn,b_mn", [(8064, 768, 3072, 0, 1), (8064, 768, 3072, 0, 0),
                                                (4096, 768, 3072, 0, 1)])
 def test_gemm_caption_dx_on_own_kernels(cuda, M, N, K, a_mn, b_mn):

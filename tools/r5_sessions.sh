@@ -99,5 +99,12 @@ r5g|r5fin|r5fin2|r5fin3)  # head check: GPU suite + smoke, the driver's default 
   done
   for w in qf lm cross linear; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -12 $O/${w}_table.txt; done
   ;;
+r5h)  # linear decoder's 8192-row N = 768 GEMMs on 128-row AGPR tiles (GVL_W4X_128=2 default) vs 0
+  ktests kt "linear_decoder_rows or test_gemm_w4x or tile128x192 or caption_dx"
+  GVL_MARGINS_DIR=$O/parity_margins ktests bench_parity "bench_shape" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for v in 2 0; do GVL_W4X_128=$v bench lin_x${v}_$r linear; done; done
+  for v in 2 0; do GVL_W4X_128=$v bench qf_x${v} qformer; done
+  for v in 2 0; do GVL_W4X_128=$v diag x$v 8192 narrow epi; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
