@@ -106,5 +106,8 @@ r5h)  # linear decoder's 8192-row N = 768 GEMMs on 128-row AGPR tiles (GVL_W4X_1
   for v in 2 0; do GVL_W4X_128=$v bench qf_x${v} qformer; done
   for v in 2 0; do GVL_W4X_128=$v diag x$v 8192 narrow epi; done
   ;;
+r5i)  # N = 768 shapes at the cross decoder's 3968 rows and the Q-Former bridge's 4096: default vs 128-row direct-A
+  for M in 3968 4096; do for v in 1 2; do GVL_W4D=$v diag w4d$v $M narrow epi; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
