@@ -221,6 +221,7 @@ void fill_params(const gvl_gemm_desc* d, GemmP& p) {
   p.nticket = d->tickets ? d->ticket_count : 0;
   p.batch = 1;
   p.grouped = 0;
+  p.alpha_mask = 0;
 }
 
 }  // namespace
@@ -497,10 +498,18 @@ extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int3
   g_batched_name[0] = 0;
   GVL_REQUIRE(d != nullptr && count >= 1, "gvl_gemm_grouped: bad arguments");
   if (count > GVL_MAX_GROUP || env().impl < 3 || env().cfg >= 0) return -1;
+  // ABI v11: one device scale for the problems that carry it (the lm_head's weight grad)
+  const void* ap = nullptr;
+  uint64_t amask = 0;
+  for (int i = 0; i < count; ++i) {
+    if (!d[i].alpha_ptr) continue;
+    if (!ap) ap = d[i].alpha_ptr;
+    amask |= uint64_t(1) << i;
+  }
   for (int i = 0; i < count; ++i) {
     const gvl_gemm_desc& e = d[i];
     if (!(e.a_mn && e.b_mn && e.residual == e.c && e.ldr == e.ldc && e.alpha == d[0].alpha &&
-          !e.alpha_ptr && !e.bias && !e.act && !e.dact && !e.gate && e.drop_p == 0.f && !e.c_fp32 &&
+          (!e.alpha_ptr || !ap || e.alpha_ptr == ap) && !e.bias && !e.act && !e.dact && !e.gate && e.drop_p == 0.f && !e.c_fp32 &&
           e.m > 0 && e.n > 0 && e.k > 0 && e.m < (1 << 30) && e.n < (1 << 30) && e.k < (1 << 30) &&
           e.lda < (1 << 30) && e.ldb < (1 << 30) && e.ldc < (1 << 30) && gvl::aligned16(e.a) && gvl::aligned16(e.b) &&
           gvl::aligned16(e.c)))
@@ -513,6 +522,8 @@ extern "C" int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int3
   p.tickets = nullptr;
   p.nticket = 0;
   p.batch = count;
+  p.alpha_ptr = static_cast<const float*>(ap);
+  p.alpha_mask = amask;
   for (int i = 0; i < GVL_MAX_GROUP; ++i) p.Db[i] = (dbias && i < count) ? dbias[i] : nullptr;
   for (int i = 0; i < count; ++i) {
     p.Ab[i] = static_cast<const bf16_t*>(d[i].a);

@@ -56,11 +56,12 @@ struct GemmP {
   // per-problem sizes / strides here (32-bit: the kernel argument block stays ~3.2 KB with 48
   // problems), gtile[i] = problem i's first work item (gtile[batch] = all)
   int grouped;
+  uint64_t alpha_mask;  // grouped: problems (bit i) whose alpha is alpha * *alpha_ptr (others: alpha)
   int32_t Mb[GVL_MAX_GROUP], Nb[GVL_MAX_GROUP], Kb[GVL_MAX_GROUP];
   int32_t ldab[GVL_MAX_GROUP], ldbb[GVL_MAX_GROUP], ldcb[GVL_MAX_GROUP];
   int gtile[GVL_MAX_GROUP + 1];
 };
-// 3152 B with 48 problems.  A kernel reads its arguments by scalar loads of the fields it uses,
+// 3160 B with 48 problems.  A kernel reads its arguments by scalar loads of the fields it uses,
 // so the per-problem tables cost the launches that never touch them only the host-side copy of
 // the block (graph replays re-use the captured copy); the bound keeps it clear of the 4 KiB limit.
 static_assert(sizeof(GemmP) <= 3584, "GemmP must stay well inside the 4 KiB kernel-argument limit");

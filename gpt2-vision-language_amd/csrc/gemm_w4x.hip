@@ -189,9 +189,10 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
   const uint32_t db_hi = (wave & 1) ? 0xFFFFFFFFu : 0u;  // odd waves sum fragments 4..7
-  // alpha x *alpha_ptr read once, before any DMA is in flight
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  // alpha x *alpha_ptr read once, before any DMA is in flight (grouped: the problems of
+  // GemmP::alpha_mask take the device scale, the others alpha alone)
+  const float alpha_dev = p.alpha_ptr ? *p.alpha_ptr : 1.f;
+  const float alpha_all = GR ? p.alpha : p.alpha * alpha_dev;
 
   float4_t acc[FM][FN];
   short8_t fa[2][FM], fb[2][FN];
@@ -230,6 +231,7 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
       ra = uniform_rsrc(p.Ab[bi], a_rows * lda_ * 2);
       rb = uniform_rsrc(p.Bb[bi], b_rows * ldb_ * 2);
     }
+    const float alpha = GR && ((p.alpha_mask >> bi) & 1) ? alpha_all * alpha_dev : alpha_all;
     bool do_db = false;
     if constexpr (DB) do_db = multi && n0 == 0 && p.Db[bi] != nullptr;
     SA::base_offsets(lda_, m0, 0, wave, lane, offa);
@@ -525,6 +527,10 @@ bool gemm_w4x_grouped_try(GemmP& p, hipStream_t s) {
   const int64_t cus = num_cus();
   auto fill = [&](int64_t tiles) { return (double)tiles / (double)(((tiles + cus - 1) / cus) * cus); };
   p.bn = fill(t256) >= 0.95 * fill(t192) ? 256 : 192;
+  // GVL_W4X_GR_BN=192|256 forces the tile width (A/B; read per call)
+  if (const char* e = getenv("GVL_W4X_GR_BN")) {
+    if (atoi(e) == 192 || atoi(e) == 256) p.bn = atoi(e);
+  }
   int t = 0;
   for (int i = 0; i < p.batch; ++i) {
     p.gtile[i] = t;

@@ -127,6 +127,9 @@ _READY_HOOKS = []
 DEFER_WGRAD = os.environ.get("GVL_DEFER_WGRAD", "1") != "0"
 DEFER_BRIDGE = os.environ.get("GVL_DEFER_BRIDGE", "1") != "0"
 DEFER_INPROJ = os.environ.get("GVL_DEFER_INPROJ", "1") != "0"  # MHAFn's packed in_proj slices too
+# The tied lm_head's weight gradient (dlogits^T x, scaled by the device scalar dloss / count) is
+# queued too (round 5), so the LM flush can group it with the blocks' (_flush_grouped)
+DEFER_LMHEAD = os.environ.get("GVL_DEFER_LMHEAD", "1") != "0"
 # Grouped flush (gvl_gemm_grouped) of the queued weight gradients of one stream over <= 8192
 # tokens: 2 (default) up to 48 problems (the cross-att decoder's 12 blocks' flush: +1.9 % on its
 # step, profiles/r4/grouped48_r4g48.txt), 1 up to 16 (the Q-Former bridge's), 0 off.  The LM's
@@ -141,7 +144,7 @@ GROUPED_MAX = 48
 # switch deferral off for later passes.  Its stale entries are dropped by discard_pending(),
 # which gvl.optim.AdamW.zero_grad calls.  Peak memory: the queued (dY, X) operands stay alive
 # until the flush.
-_PENDING = []          # (task, param, grad sink, dy2, x2, stream)
+_PENDING = []          # (task, param, grad sink, dy2, x2, stream, alpha_ptr or None)
 _PENDING_B = []        # (task, param, grad sink, dy2, stream): bias gradients = column sums of dy2
 _QUEUED = set()        # graph tasks with a flush callback queued
 # Data-parallel overlap (gvl.dist.GradBuckets sets it for the synchronising micro-step):
@@ -210,7 +213,7 @@ def flush_wgrads(task=None):
     paired = {}
     rest_b = []
     if pend_b and pend:
-        wkeys = {_dkey(d) for _, _, d, _, _ in pend}
+        wkeys = {_dkey(d) for _, _, d, _, _, _ in pend}
         for p, g, dy2, st in pend_b:
             k = _dkey(dy2)
             if k in wkeys and k not in paired:
@@ -220,9 +223,10 @@ def flush_wgrads(task=None):
     else:
         rest_b = pend_b
     groups = {}
-    for p, g, dy2, x2, st in pend:
+    for p, g, dy2, x2, st, ap in pend:
+        # key[-2]: the device scale of the problem (the tied lm_head's, else None), key[-1]: stream
         key = (tuple(dy2.shape), dy2.stride(0), tuple(x2.shape), x2.stride(0), g.stride(0),
-               dy2.device, st)
+               dy2.device, ap, st)
         groups.setdefault(key, []).append((p, g, dy2, x2))
     if GROUPED_WGRAD and len(groups) >= 2:
         groups = _flush_grouped(groups, paired, _done)
@@ -230,6 +234,11 @@ def flush_wgrads(task=None):
     ready = []
     for key, items in order:
         with torch.cuda.stream(key[-1]):
+            if key[-2] is not None:  # scaled by a device scalar: one launch each
+                for p, g, dy2, x2 in items:
+                    K.gemm(dy2, x2, a_mn=True, b_mn=True, alpha_ptr=key[-2], out=g, residual=g)
+                    ready.append(p)
+                items = []
             for i in range(0, len(items), 16):
                 chunk = items[i:i + 16]
                 bias = [paired.pop(_dkey(d), None) for _, _, d, _ in chunk]
@@ -264,29 +273,69 @@ def flush_wgrads(task=None):
                         _done(p)
 
 
+_CUS = {}
+
+
+def _num_cus(dev):
+    if dev not in _CUS:
+        _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CUS[dev]
+
+
+def _tiles256(its):
+    """256 x 256 output tiles of one problem of a shape group (dW [M, N] = dY^T X)."""
+    _, _, dy2, x2 = its[0]
+    return -(-dy2.shape[1] // 256) * -(-x2.shape[1] // 256)
+
+
 def _flush_grouped(groups, paired, done):
-    """Every queued weight gradient of the flush as one grouped launch when they share a stream,
-    run over at most 8192 tokens and number at most GROUPED_MAX (GROUPED_WGRAD 1: 16); returns
-    the groups left to the per-shape path."""
+    """Queued weight gradients of one stream as one grouped launch (gvl_gemm_grouped); returns
+    the groups left to the per-shape path.
+    * Flushes over <= 8192 tokens (the caption steps): all of them, at most GROUPED_MAX
+      (GROUPED_WGRAD 1: 16).
+    * Larger ones (the LM's 16k-token micro-step, GROUPED_WGRAD 2): the shapes of >= 16 tiles per
+      problem (c_attn, c_fc, mlp.c_proj and the tied lm_head's dW, scaled by its device scalar),
+      when one launch over all their tiles takes fewer whole rounds of CUs than the per-shape
+      launches (each a whole number of rounds; under one round they split K), counting the
+      grouped launch's tiles 10 % slower (profiles/r5/lm_wgrad_grouped_r5k.txt: 3713 vs 3966 us
+      for the 37 problems).  The small attn.c_proj problems keep their split-K batch."""
+    if len({key[-1] for key in groups}) != 1:
+        return groups
     items = [it for its in groups.values() for it in its]
-    if len({key[-1] for key in groups}) != 1 or any(it[2].shape[0] > 8192 for it in items):
-        return groups
-    if len(items) > (GROUPED_MAX if GROUPED_WGRAD >= 2 else 16):
-        return groups
-    bias = [paired.pop(_dkey(d), None) for _, _, d, _ in items]
+    if all(it[2].shape[0] <= 8192 for it in items):
+        if len(items) > (GROUPED_MAX if GROUPED_WGRAD >= 2 else 16):
+            return groups
+        sel = groups
+    else:
+        if GROUPED_WGRAD < 2:
+            return groups
+        sel = {k: its for k, its in groups.items() if _tiles256(its) >= 16}
+        n = sum(len(its) for its in sel.values())
+        if len(sel) < 2 or n > GROUPED_MAX:
+            return groups
+        cus = _num_cus(items[0][2].device)
+        sep = 0.0
+        for its in sel.values():
+            t = _tiles256(its) * len(its)
+            sep += t / cus if t < cus else -(-t // cus)
+        tot = -(-sum(_tiles256(its) * len(its) for its in sel.values()) // cus)
+        if tot * 1.1 >= sep:
+            return groups
+    entries = [(it, key[-2]) for key, its in sel.items() for it in its]
+    bias = [paired.pop(_dkey(it[2]), None) for it, _ in entries]
     with torch.cuda.stream(next(iter(groups))[-1]):
-        ok = K.gemm_grouped([(dy2, x2, g) for _, g, dy2, x2 in items],
+        ok = K.gemm_grouped([(dy2, x2, g, ap) for (_, g, dy2, x2), ap in entries],
                             dbias=[b[1] if b is not None else None for b in bias])
     if not ok:
-        for (_, _, d, _), b in zip(items, bias):
+        for (it, _), b in zip(entries, bias):
             if b is not None:
-                paired[_dkey(d)] = b
+                paired[_dkey(it[2])] = b
         return groups
-    for (p, _, _, _), b in zip(items, bias):
+    for ((p, _, _, _), _), b in zip(entries, bias):
         done(p)
         if b is not None:
             done(b[0])
-    return {}
+    return {k: its for k, its in groups.items() if k not in sel}
 
 
 def _final_flush(task):
@@ -294,13 +343,13 @@ def _final_flush(task):
     flush_wgrads(task)
 
 
-def _defer_wgrad(p, g, dy2, x2):
+def _defer_wgrad(p, g, dy2, x2, alpha_ptr=None):
     task = _task()
     p._gvl_sunk_task = task
     if x2 is None:  # bias gradient
         _PENDING_B.append((task, p, g, dy2, torch.cuda.current_stream(dy2.device)))
     else:
-        _PENDING.append((task, p, g, dy2, x2, torch.cuda.current_stream(dy2.device)))
+        _PENDING.append((task, p, g, dy2, x2, torch.cuda.current_stream(dy2.device), alpha_ptr))
     if task not in _QUEUED:
         _QUEUED.add(task)
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _final_flush(task))
@@ -1059,7 +1108,11 @@ class LMHeadLossFn(torch.autograd.Function):
             else:
                 xt = x2.view(B, S, C)[:, off:off + T].reshape(B * T, C).contiguous()
             g = _sink(ctx.params[1], ctx)  # the tied wte's arena gradient: C += dl^T x
-            if g is not None:
+            if g is not None and DEFER_WGRAD and DEFER_LMHEAD:
+                # queued: the end-of-backward flush can run it in one grouped launch with the
+                # blocks' weight gradients (dl and xt stay alive in the queue until then)
+                _defer_wgrad(ctx.params[1], g, dl, xt, alpha_ptr=scale)
+            elif g is not None:
                 K.gemm(dl, xt, a_mn=True, b_mn=True, alpha_ptr=scale, out=g, residual=g)
                 _ready(ctx.params[1])
             else:

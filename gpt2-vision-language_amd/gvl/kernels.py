@@ -283,14 +283,19 @@ def gemm_batched(items, *, a_mn=False, b_mn=False, dbias=None):
 def gemm_grouped(items, dbias=None):
     """Weight gradients of different shapes as ONE launch (gvl_gemm_grouped): items =
     [(dy, x, out)], out += dy^T @ x (dy [K_i, M_i], x [K_i, N_i], out [M_i, N_i], bf16,
-    MN-contiguous operands); dbias: None or a list with a bf16 [M_i] bias grad or None per
-    item, += column sums of dy_i.  Returns False when nothing was launched (the caller runs
-    the problems another way)."""
+    MN-contiguous operands); an item may carry a 4th element, an fp32 device scalar (or None)
+    its product is scaled by (ABI v11: one such tensor per call); dbias: None or a list with a
+    bf16 [M_i] bias grad or None per item, += column sums of dy_i.  Returns False when nothing
+    was launched (the caller runs the problems another way)."""
     n = len(items)
     if n == 0:
         return True
     arr = (GemmDesc * n)()
-    for i, (a, b, out) in enumerate(items):
+    for i, it in enumerate(items):
+        a, b, out = it[:3]
+        ap = it[3] if len(it) > 3 else None
+        if ap is not None and (ap.dtype != torch.float32 or not ap.is_cuda):
+            raise TypeError("gvl.gemm_grouped: alpha_ptr must be an fp32 device tensor")
         _dev(a, b)
         _rowmajor(a, "A")
         _rowmajor(b, "B")
@@ -305,6 +310,7 @@ def gemm_grouped(items, dbias=None):
         d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), out.stride(0)
         d.a_mn, d.b_mn = 1, 1
         d.alpha = 1.0
+        d.alpha_ptr = _p(ap)
         d.residual, d.ldr = out.data_ptr(), out.stride(0)
     da = None
     if dbias is not None:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 10
+#define GVL_ABI_VERSION 11
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -111,6 +111,10 @@ int gvl_gemm_batched_dbias(const gvl_gemm_desc* d, void* const* dbias, int32_t c
  * alpha; dbias[i] (bf16 [m], may be null; the array may be null) += column sums of dY_i.
  * count <= 48 (round 4: also every GPT-2 block's four weight grads of one LM backward flush,
  * train_gpt2.py:55-59,71-74, sizes and strides < 2^30).
+ * ABI v11: a problem's alpha_ptr may be set (the tied lm_head's weight grad, scaled by the
+ * device scalar dloss / count, train_gpt2.py:469 + the reference's loss scaling): every non-null
+ * alpha_ptr of one call must be the same pointer; those problems get alpha * *alpha_ptr, the
+ * others alpha.
  * Returns 0 when launched, -1 when the problems do not qualify and nothing was launched. */
 int gvl_gemm_grouped(const gvl_gemm_desc* d, void* const* dbias, int32_t count,
                      gvl_stream_t stream);

@@ -887,6 +887,38 @@ def test_gemm_grouped_wgrad(cuda, shapes):
             assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
 
 
+def test_gemm_grouped_device_scale(cuda):
+    """ABI v11: a grouped launch where some problems carry the device scalar (the tied lm_head's
+    dW, scaled by dloss / count: a 50304-row problem, shrunk here to 2000 rows) and the others
+    none; each vs its fp32 reference.  Two different scale tensors in one call are declined."""
+    K_ = _k()
+    torch.manual_seed(11)
+    shapes = [(1024, 2000, 768), (1024, 768, 3072), (1024, 3072, 768), (1024, 2304, 768)]
+    dys = [(torch.randn(k, m) * 0.1).to(BF) for k, m, n in shapes]
+    xs = [(torch.randn(k, n) * 0.1).to(BF) for k, m, n in shapes]
+    c0 = [torch.randn(m, n).to(BF) for k, m, n in shapes]
+    b0 = [torch.randn(m).to(BF) for k, m, n in shapes]
+    scale = torch.tensor([0.37], device=cuda)
+    outs = [c.to(cuda) for c in c0]
+    dbs = [None] + [b.to(cuda) for b in b0[1:]]
+    items = [(dy.to(cuda), x.to(cuda), o, scale if i == 0 else None)
+             for i, (dy, x, o) in enumerate(zip(dys, xs, outs))]
+    assert K_.gemm_grouped(items, dbias=dbs)
+    torch.cuda.synchronize()
+    for i, (dy, x, c, o, b, db) in enumerate(zip(dys, xs, c0, outs, b0, dbs)):
+        a = 0.37 if i == 0 else 1.0
+        ref = a * (dy.float().t() @ x.float()) + c.float()
+        assert rel_err(o.float().cpu().numpy(), ref.numpy()) < 8e-3, i
+        if db is not None:
+            assert rel_err(db.float().cpu().numpy(), (dy.float().sum(0) + b.float()).numpy()) < 1e-2
+    other = torch.tensor([2.0], device=cuda)
+    before = [o.clone() for o in outs]
+    assert not K_.gemm_grouped([items[0], items[1][:3] + (other,)])
+    torch.cuda.synchronize()
+    for o, b in zip(outs, before):
+        assert torch.equal(o, b)
+
+
 def test_gemm_grouped_declines_past_limit(cuda):
     """gvl_gemm_grouped returns -1 (gemm_grouped False) for 49 problems, launching nothing."""
     K_ = _k()

@@ -109,5 +109,29 @@ r5h)  # linear decoder's 8192-row N = 768 GEMMs on 128-row AGPR tiles (GVL_W4X_1
 r5i)  # N = 768 shapes at the cross decoder's 3968 rows and the Q-Former bridge's 4096: default vs 128-row direct-A
   for M in 3968 4096; do for v in 1 2; do GVL_W4D=$v diag w4d$v $M narrow epi; done; done
   ;;
+r5j)  # wide K = 768 GEMMs: row sweep (fixed vs per-tile cost), shipped / d1 (plain stores) / d2 (no stores); attention G A/B
+  for L in base d1 d2; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 240 python -u tools/pp3_sweep.py > $O/sweep_$L.log 2>&1; fatal $? sweep_$L
+    echo "== $L"; cat $O/sweep_$L.log
+  done
+  for r in 1 2; do for G in 0 1; do
+    if [ $G = 1 ]; then export GVL_ATTN_G=1; else unset GVL_ATTN_G; fi
+    timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_g${G}_$r.log 2>&1; fatal $? attn
+    echo "attn G=$G $r"; grep "B=" $O/attn_g${G}_$r.log | head -2
+  done; done
+  unset GVL_ATTN_G
+  ;;
+r5k)  # LM weight gradients: c_attn / c_fc / mlp.c_proj batches + the lm_head dW as ONE grouped launch (whole rounds)
+  GVL_WGRAD_LM=1 timeout -k 10 400 python -u tools/wgrad_diag.py > $O/wgrad_lm.log 2>&1; rc=$?; cat $O/wgrad_lm.log | grep -v amdgpu.ids; fatal $rc wgrad
+  ;;
+r5l)  # the tied lm_head's dW deferred and grouped with the blocks' (ABI v11 device scale per problem)
+  ktests kt "grouped or w4x or wgrad"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "lm" tests/test_gpu_parity_full.py
+  ktests dp "lm or overlap" tests/test_gpu_dp.py
+  ktests bnd "" tests/test_gpu_boundary.py
+  for r in 1 2; do for v in 1 0; do GVL_DEFER_LMHEAD=$v bench lm_d${v}_$r lm; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac

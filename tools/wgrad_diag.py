@@ -68,3 +68,40 @@ _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
 tg = timeit(lambda: K.gemm_grouped(gitems, dbias=gdb))
 print(f"grouped x{len(gitems)} (+dbias): {tg:8.1f}us ({tot_fl / tg / 1e6:6.0f} TF/s)  vs the four batches "
       f"{tot_b:8.1f}us ({tot_fl / tot_b / 1e6:6.0f} TF/s)  [{buf.value.decode()}]", flush=True)
+
+# The tied lm_head's weight gradient (dW = dlogits^T x over the micro-step's tokens, 50304 x 768)
+# alone, and grouped with the 36 c_attn / c_fc / mlp.c_proj problems (GVL_WGRAD_LM=1): whole
+# rounds of CUs across all of them instead of per-batch partial last rounds.
+if os.environ.get("GVL_WGRAD_LM", "0") == "1":
+    V = 50304
+    dl = (torch.rand(KT, V, device=dev) - 0.5).to(torch.bfloat16)
+    xl = (torch.rand(KT, 768, device=dev) - 0.5).to(torch.bfloat16)
+    gl = torch.zeros(V, 768, device=dev, dtype=torch.bfloat16)
+    fl_lm = 2.0 * V * 768 * KT
+    t_lm = timeit(lambda: K.gemm(dl, xl, a_mn=True, b_mn=True, out=gl, residual=gl))
+    print(f"lm_head dW   M={V} N=768 K={KT}: {t_lm:8.1f}us ({fl_lm / t_lm / 1e6:6.0f} TF/s)", flush=True)
+    sel = [0, 2, 3]  # c_attn, c_fc, mlp.c_proj
+    fl_sel = sum(2.0 * SHAPES[s][1] * SHAPES[s][2] * KT * L for s in sel) + fl_lm
+    blk = [(ALL[s][0][i], ALL[s][1][i], ALL[s][2][i]) for s in sel for i in range(L)]
+    blk_db = [ALL[s][3][i] for s in sel for i in range(L)]
+    tsep = {}
+    for s in sel:
+        items = [(ALL[s][0][i], ALL[s][1][i], ALL[s][2][i], True) for i in range(L)]
+        tsep[s] = timeit(lambda: K.gemm_batched(items, a_mn=True, b_mn=True, dbias=ALL[s][3]))
+    sep = sum(tsep.values()) + t_lm
+    print(f"separate: batches {' + '.join(f'{tsep[s]:.1f}' for s in sel)} + lm_head {t_lm:.1f} = {sep:8.1f}us "
+          f"({fl_sel / sep / 1e6:6.0f} TF/s)", flush=True)
+    for order in ("lm_last", "lm_first"):
+        its = blk + [(dl, xl, gl)] if order == "lm_last" else [(dl, xl, gl)] + blk
+        dbs = blk_db + [None] if order == "lm_last" else [None] + blk_db
+        for bn in ("auto", "256", "192"):
+            if bn == "auto":
+                os.environ.pop("GVL_W4X_GR_BN", None)
+            else:
+                os.environ["GVL_W4X_GR_BN"] = bn
+            assert K.gemm_grouped(its, dbias=dbs)
+            _lib.lib().gvl_gemm_batched_kernel_name(buf, 128)
+            tg = timeit(lambda: K.gemm_grouped(its, dbias=dbs))
+            print(f"grouped x{len(its)} {order} bn={bn}: {tg:8.1f}us ({fl_sel / tg / 1e6:6.0f} TF/s)  "
+                  f"[{buf.value.decode()}]", flush=True)
+    os.environ.pop("GVL_W4X_GR_BN", None)
