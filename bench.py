@@ -290,7 +290,7 @@ def dominant_kernel(summary, workload="lm", steps=1):
     events bound to each kernel's own dispatch (gvl.kernels.KernelTimer, dispatch=True):
     the interval rocprofv3's kernel trace reports for the same kernel name.  Also lists the
     top GEMM instances (per-step launches, average duration, fraction of peak).  Every GEMM
-    is one of libgvl's own kernels (ABI v10: no vendor-library route)."""
+    is one of libgvl's own kernels (since ABI v10: no vendor-library route)."""
     name, s = max(summary.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = s["ms"] / s["launches"]
     achieved = s["flops"] / (s["ms"] * 1e-3) / 1e12

@@ -133,5 +133,8 @@ r5l)  # the tied lm_head's dW deferred and grouped with the blocks' (ABI v11 dev
   ktests bnd "" tests/test_gpu_boundary.py
   for r in 1 2; do for v in 1 0; do GVL_DEFER_LMHEAD=$v bench lm_d${v}_$r lm; done; done
   ;;
+r5m)  # wide K = 768 plain products on the AGPR four-wave kernel (GVL_W4X=2) vs the persistent kernel
+  for v in 1 2 1 2; do GVL_W4X=$v timeout -k 10 240 python -u tools/pp3_sweep.py > $O/sweep_w4x$v.log 2>&1; fatal $? sweep; echo "== GVL_W4X=$v"; grep -v amdgpu.ids $O/sweep_w4x$v.log; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
