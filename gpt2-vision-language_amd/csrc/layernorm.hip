@@ -242,6 +242,44 @@ __global__ __launch_bounds__(1024) void ln_bwd_finalize(const float* __restrict_
   *dst = f2bf(t);
 }
 
+// Batched form (gvl_layernorm_bwd_finalize_batched): blockIdx.y = item, each item as above.
+constexpr int LN_FIN_MAX = 64;
+struct LnFinBatch {
+  const float* ws[LN_FIN_MAX];
+  bf16_t* dw[LN_FIN_MAX];
+  bf16_t* db[LN_FIN_MAX];
+  int nblk[LN_FIN_MAX];
+};
+__global__ __launch_bounds__(1024) void ln_bwd_finalize_batched(LnFinBatch b, int C, int acc) {
+  __shared__ float red[64][17];
+  const int it = blockIdx.y;
+  const float* __restrict__ ws = b.ws[it];
+  const int nblk = b.nblk[it];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float s = 0.f;
+  if (c < 2 * C) {
+    float v[LN_BWD_MAXB / 64];
+#pragma unroll
+    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) {
+      const int k = g + 64 * j;
+      v[j] = k < nblk ? ws[(int64_t)k * 2 * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) s += v[j];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (threadIdx.x >= 16 || c >= 2 * C) return;
+  float t = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) t += red[k][cl];
+  bf16_t* dst = (c < C) ? (b.dw[it] ? b.dw[it] + c : nullptr) : (b.db[it] ? b.db[it] + (c - C) : nullptr);
+  if (!dst) return;
+  if (acc) t += bf2f(*dst);
+  *dst = f2bf(t);
+}
+
 // >= 2 rows per wave, <= LN_BWD_MAXB blocks (512: 2 per CU, 8 waves, ~16 rows in flight per CU).
 int ln_bwd_blocks(int64_t rows) {
   int64_t nb = (rows + 7) / 8;
@@ -294,11 +332,14 @@ static int ln_bwd_launch(const void* dy, int64_t lddy, const void* x, int64_t ld
                   gvl::aligned16(w) && (!accumulate_dx || (ldr % 8 == 0 && gvl::aligned16(res))),
               "gvl_layernorm_bwd: cols unsupported (need cols %% 8 == 0, <= 1024, ld %% 8 == 0, "
               "16-byte aligned rows)");
-  GVL_REQUIRE(!(dw || db) || workspace, "gvl_layernorm_bwd: dw/db need a workspace");
+  // accumulate_wb bit 1 (ABI v12): leave the column partials in the workspace for a later
+  // gvl_layernorm_bwd_finalize_batched (dw / db are not touched here)
+  const bool defer = (accumulate_wb & 2) != 0;
+  GVL_REQUIRE(!(dw || db || defer) || workspace, "gvl_layernorm_bwd: dw/db need a workspace");
   if (rows == 0) return 0;
   const int nb = ln_bwd_blocks(rows);
   hipStream_t s = gvl::as_stream(stream);
-  float* ws = (dw || db) ? static_cast<float*>(workspace) : nullptr;
+  float* ws = (dw || db || defer) ? static_cast<float*>(workspace) : nullptr;
   const auto dyp = static_cast<const bf16_t*>(dy);
   const auto xp = static_cast<const bf16_t*>(x);
   const auto wp = static_cast<const bf16_t*>(w);
@@ -311,7 +352,7 @@ static int ln_bwd_launch(const void* dy, int64_t lddy, const void* x, int64_t ld
     hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(LN_BWD_NT), 0, s, dyp, lddy, xp, ldx, wp,
                        mean, rstd, rp, ldr, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd");
-  if (ws) {
+  if (ws && !defer) {
     const int g2 = (int)((2 * cols + 15) / 16);
     hipLaunchKernelGGL(ln_bwd_finalize, dim3(g2), dim3(1024), 0, s, ws, nb, (int)cols,
                        static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), (int)accumulate_wb);
@@ -337,4 +378,30 @@ extern "C" int gvl_layernorm_bwd_res(const void* dy, int64_t lddy, const void* x
   GVL_REQUIRE(res != nullptr, "gvl_layernorm_bwd_res: null residual");
   return ln_bwd_launch(dy, lddy, x, ldx, w, mean, rstd, res, ldr, dx, lddx, 1, dw, db,
                        accumulate_wb, workspace, rows, cols, stream);
+}
+
+extern "C" int32_t gvl_layernorm_bwd_blocks(int64_t rows) { return rows > 0 ? ln_bwd_blocks(rows) : 0; }
+
+extern "C" int gvl_layernorm_bwd_finalize_batched(const float* const* ws, const int32_t* nblk,
+                                                  int32_t count, int64_t cols, void* const* dw,
+                                                  void* const* db, int32_t accumulate_wb,
+                                                  gvl_stream_t stream) {
+  GVL_REQUIRE(ws && nblk && count >= 0 && count <= LN_FIN_MAX && cols > 0 && cols <= 1024,
+              "gvl_layernorm_bwd_finalize_batched: bad arguments (count <= %d, cols <= 1024)",
+              LN_FIN_MAX);
+  if (count == 0) return 0;
+  LnFinBatch b{};
+  for (int i = 0; i < count; ++i) {
+    GVL_REQUIRE(ws[i] != nullptr && nblk[i] >= 0 && nblk[i] <= LN_BWD_MAXB,
+                "gvl_layernorm_bwd_finalize_batched: item %d: null workspace or bad block count", i);
+    b.ws[i] = ws[i];
+    b.nblk[i] = nblk[i];
+    b.dw[i] = dw ? static_cast<bf16_t*>(dw[i]) : nullptr;
+    b.db[i] = db ? static_cast<bf16_t*>(db[i]) : nullptr;
+  }
+  const int g2 = (int)((2 * cols + 15) / 16);
+  hipLaunchKernelGGL(ln_bwd_finalize_batched, dim3(g2, count), dim3(1024), 0, gvl::as_stream(stream), b,
+                     (int)cols, (int)(accumulate_wb & 1));
+  GVL_LAUNCH_CHECK("gvl_layernorm_bwd_finalize_batched");
+  return 0;
 }

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 11  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 12  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -79,6 +79,9 @@ SIGNATURES = {
     "gvl_layernorm_fwd": (C.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                     c_i64, c_i64, c_f32, c_vp]),
     "gvl_layernorm_bwd_workspace_size": (c_i64, [c_i64, c_i64]),
+    "gvl_layernorm_bwd_blocks": (c_i32, [c_i64]),
+    "gvl_layernorm_bwd_finalize_batched": (C.c_int, [C.POINTER(c_vp), C.POINTER(c_i32), c_i32, c_i64,
+                                                     C.POINTER(c_vp), C.POINTER(c_vp), c_i32, c_vp]),
     "gvl_layernorm_bwd": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
                                     c_i32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp]),
     "gvl_layernorm_bwd_res": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,

@@ -130,6 +130,10 @@ DEFER_INPROJ = os.environ.get("GVL_DEFER_INPROJ", "1") != "0"  # MHAFn's packed 
 # The tied lm_head's weight gradient (dlogits^T x, scaled by the device scalar dloss / count) is
 # queued too (round 5), so the LM flush can group it with the blocks' (_flush_grouped)
 DEFER_LMHEAD = os.environ.get("GVL_DEFER_LMHEAD", "1") != "0"
+# LayerNorm weight / bias gradients (round 5, ABI v12): the backward leaves its per-block column
+# partials in a workspace and the flush reduces all of them in one launch
+# (gvl_layernorm_bwd_finalize_batched) instead of one finalize launch per LayerNorm
+DEFER_LN = os.environ.get("GVL_DEFER_LN", "1") != "0"
 # Grouped flush (gvl_gemm_grouped) of the queued weight gradients of one stream over <= 8192
 # tokens: 2 (default) up to 48 problems (the cross-att decoder's 12 blocks' flush: +1.9 % on its
 # step, profiles/r4/grouped48_r4g48.txt), 1 up to 16 (the Q-Former bridge's), 0 off.  The LM's
@@ -146,6 +150,7 @@ GROUPED_MAX = 48
 # until the flush.
 _PENDING = []          # (task, param, grad sink, dy2, x2, stream, alpha_ptr or None)
 _PENDING_B = []        # (task, param, grad sink, dy2, stream): bias gradients = column sums of dy2
+_PENDING_LN = []       # (task, w, b, grad sink w or None, grad sink b or None, workspace, blocks, cols, stream)
 _QUEUED = set()        # graph tasks with a flush callback queued
 # Data-parallel overlap (gvl.dist.GradBuckets sets it for the synchronising micro-step):
 # with OVERLAP_BLOCKS[0] = G > 0 every G-th GPT-2 block backward flushes its task's queue in
@@ -169,6 +174,7 @@ def discard_pending():
     """Drop every queued deferred gradient (left behind by a backward that raised)."""
     _PENDING.clear()
     _PENDING_B.clear()
+    _PENDING_LN.clear()
     _QUEUED.clear()
     _BLOCKS_SEEN.clear()
 
@@ -194,17 +200,36 @@ def flush_wgrads(task=None):
     that queued any; harmless when empty."""
     pend = [e[1:] for e in _take(_PENDING, task)]
     pend_b = [e[1:] for e in _take(_PENDING_B, task)]
+    pend_ln = [e[1:] for e in _take(_PENDING_LN, task)]
     _BLOCKS_SEEN.pop(task, None)
     # a parameter may have several queued entries (the packed in_proj's row slices): its
     # grad-ready hook runs once, after the last of them is launched
     left = {}
     for e in pend + pend_b:
         left[id(e[0])] = left.get(id(e[0]), 0) + 1
+    for w, b, gw, gb, *_ in pend_ln:
+        for p, g in ((w, gw), (b, gb)):
+            if g is not None:
+                left[id(p)] = left.get(id(p), 0) + 1
 
     def _done(p):
         left[id(p)] -= 1
         if left[id(p)] == 0:
             _ready(p)
+
+    if pend_ln:
+        lgroups = {}
+        for w, b, gw, gb, ws, nblk, cols, st in pend_ln:
+            lgroups.setdefault((cols, st), []).append((w, b, gw, gb, ws, nblk))
+        for (cols, st), its in lgroups.items():
+            with torch.cuda.stream(st):
+                K.layernorm_finalize_batched([(ws, nblk, gw, gb) for _, _, gw, gb, ws, nblk in its],
+                                             cols, accumulate=True)
+            for w, b, gw, gb, _, _ in its:
+                if gw is not None:
+                    _done(w)
+                if gb is not None:
+                    _done(b)
 
     # a bias gradient over the same dY as a queued weight gradient rides in that batched GEMM
     # (gvl_gemm_batched_dbias: row sums of dY^T from the same operand tiles); each bias pairs
@@ -343,6 +368,12 @@ def _final_flush(task):
     flush_wgrads(task)
 
 
+def _queue_flush(task):
+    if task not in _QUEUED:
+        _QUEUED.add(task)
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _final_flush(task))
+
+
 def _defer_wgrad(p, g, dy2, x2, alpha_ptr=None):
     task = _task()
     p._gvl_sunk_task = task
@@ -350,9 +381,7 @@ def _defer_wgrad(p, g, dy2, x2, alpha_ptr=None):
         _PENDING_B.append((task, p, g, dy2, torch.cuda.current_stream(dy2.device)))
     else:
         _PENDING.append((task, p, g, dy2, x2, torch.cuda.current_stream(dy2.device), alpha_ptr))
-    if task not in _QUEUED:
-        _QUEUED.add(task)
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _final_flush(task))
+    _queue_flush(task)
 
 
 def _block_done():
@@ -460,6 +489,17 @@ def _ln_bwd(ctx, iw, ib, w, b, dy2, x2, mean, rstd, dx, accumulate_dx, residual=
     gw = _sink(w, ctx) if nw else None
     gb = _sink(b, ctx) if nb else None
     if (nw or nb) and (gw is not None or not nw) and (gb is not None or not nb):
+        if DEFER_WGRAD and DEFER_LN and x2.shape[0] > 0:  # partials flushed at the end of backward
+            _, (ws, nblk) = K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx,
+                                            residual=residual, defer_wb=True)
+            task = _task()
+            for p, n in ((w, nw), (b, nb)):
+                if n:
+                    p._gvl_sunk_task = task
+            _PENDING_LN.append((task, w, b, gw, gb, ws, nblk, x2.shape[1],
+                                torch.cuda.current_stream(x2.device)))
+            _queue_flush(task)
+            return None, None
         K.layernorm_bwd(dy2, x2, w, mean, rstd, dx=dx, accumulate_dx=accumulate_dx, dw=gw, db=gb,
                         accumulate_wb=True, residual=residual)
         for p, n in ((w, nw), (b, nb)):

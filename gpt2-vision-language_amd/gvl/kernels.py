@@ -355,29 +355,51 @@ def layernorm_fwd(x2, w, b, eps=1e-5, out=None, stats=True):
 
 
 def layernorm_bwd(dy2, x2, w, mean, rstd, dx=None, accumulate_dx=False, dw=None, db=None,
-                  accumulate_wb=False, residual=None):
+                  accumulate_wb=False, residual=None, defer_wb=False):
     """dx [= dx | residual] + LayerNorm backward; `residual` (a [rows, cols] bf16 operand read
-    instead of dx, gvl_layernorm_bwd_res) saves the caller a copy of the residual gradient."""
+    instead of dx, gvl_layernorm_bwd_res) saves the caller a copy of the residual gradient.
+    defer_wb (ABI v12): the dw / db column sums are left as per-block partials; returns
+    (dx, (workspace, blocks)) for a later layernorm_finalize_batched."""
     rows, cols = x2.shape
     if dx is None:
         dx = torch.empty(rows, cols, dtype=BF16, device=x2.device)
     ws = None
-    if dw is not None or db is not None:
+    if dw is not None or db is not None or defer_wb:
         n = _L().gvl_layernorm_bwd_workspace_size(rows, cols)
         ws = torch.empty(max(n, 4) // 4, dtype=F32, device=x2.device)
+    if defer_wb:
+        dw = db = None
+        accumulate_wb = 2
     if residual is not None:
         _lib.check(_L().gvl_layernorm_bwd_res(
             dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
             mean.data_ptr(), rstd.data_ptr(), residual.data_ptr(), residual.stride(0),
             dx.data_ptr(), dx.stride(0), _p(dw), _p(db), int(accumulate_wb), _p(ws), rows, cols,
             _stream()), "gvl_layernorm_bwd_res")
-        return dx
-    _lib.check(_L().gvl_layernorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
-                                      w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
-                                      dx.stride(0), int(accumulate_dx), _p(dw), _p(db),
-                                      int(accumulate_wb), _p(ws), rows, cols, _stream()),
-               "gvl_layernorm_bwd")
+    else:
+        _lib.check(_L().gvl_layernorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0),
+                                          w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                          dx.stride(0), int(accumulate_dx), _p(dw), _p(db),
+                                          int(accumulate_wb), _p(ws), rows, cols, _stream()),
+                   "gvl_layernorm_bwd")
+    if defer_wb:
+        return dx, (ws, int(_L().gvl_layernorm_bwd_blocks(rows)))
     return dx
+
+
+def layernorm_finalize_batched(items, cols, accumulate=True):
+    """The deferred LayerNorm weight / bias gradients of one width: items = [(workspace,
+    blocks, dw or None, db or None)] from layernorm_bwd(defer_wb=True); one launch per 64."""
+    for i in range(0, len(items), 64):
+        chunk = items[i:i + 64]
+        n = len(chunk)
+        ws = (C.c_void_p * n)(*[t[0].data_ptr() for t in chunk])
+        nb = (C.c_int32 * n)(*[t[1] for t in chunk])
+        dw = (C.c_void_p * n)(*[_p(t[2]) for t in chunk])
+        db = (C.c_void_p * n)(*[_p(t[3]) for t in chunk])
+        _lib.check(_L().gvl_layernorm_bwd_finalize_batched(ws, nb, n, int(cols), dw, db,
+                                                           int(bool(accumulate)), _stream()),
+                   "gvl_layernorm_bwd_finalize_batched")
 
 
 # ------------------------------------------------------------------------- attention

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 11
+#define GVL_ABI_VERSION 12
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -159,6 +159,17 @@ int gvl_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx,
                       void* dx, int64_t lddx, int32_t accumulate_dx,
                       void* dw, void* db, int32_t accumulate_wb, void* workspace,
                       int64_t rows, int64_t cols, gvl_stream_t stream);
+/* ABI v12: accumulate_wb bit 1 (value 2 | accumulate) defers the dw / db column sums: the
+ * per-block partials stay in `workspace` (gvl_layernorm_bwd_blocks(rows) blocks of 2 * cols
+ * floats) and dw / db are left untouched; one gvl_layernorm_bwd_finalize_batched launch later
+ * reduces up to 64 such workspaces of one width into their dw[i] / db[i] (either may be null),
+ * adding into them when accumulate_wb bit 0 is set — the end-of-backward flush of every
+ * LayerNorm weight grad of a GPT-2 micro-step (train_gpt2.py:66,68,94) in one launch instead
+ * of 25. */
+int32_t gvl_layernorm_bwd_blocks(int64_t rows);
+int gvl_layernorm_bwd_finalize_batched(const float* const* ws, const int32_t* nblk, int32_t count,
+                                       int64_t cols, void* const* dw, void* const* db,
+                                       int32_t accumulate_wb, gvl_stream_t stream);
 /* dx = res + LayerNorm backward (the residual-stream gradient of a pre-LN block:
  * source/gpt2/train_gpt2.py:72-73, x + attn(ln_1(x)) / x + mlp(ln_2(x))) with the residual
  * read from its own buffer, so the caller needs no copy of it; otherwise as above. */

@@ -987,6 +987,22 @@ def test_layernorm_fwd_bwd(cuda, rows, C):
     K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd, dx=dx2, residual=prev_d)
     assert rel_err(dx2.float().cpu().numpy(), (xr.grad + prev.float()).numpy()) < 1e-2
     assert torch.equal(prev_d.cpu(), prev)
+    # ABI v12: dw / db left as partials, reduced later by the batched finalize (two items: this
+    # LayerNorm's and a second one over the first half of the rows, db only), bit-identical to
+    # the in-place finalize
+    dx3, (ws, nblk) = K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd,
+                                       residual=prev_d, defer_wb=True)
+    assert torch.equal(dx3, dx2)
+    h = max(rows // 2, 1)
+    _, (ws2, nblk2) = K_.layernorm_bwd(dy[:h].to(cuda), x[:h].to(cuda), w.to(cuda), mean[:h], rstd[:h],
+                                       defer_wb=True)
+    dwb, dbb = dw0.to(BF).to(cuda), db0.to(BF).to(cuda)
+    db2 = torch.zeros(C, dtype=BF, device=cuda)
+    K_.layernorm_finalize_batched([(ws, nblk, dwb, dbb), (ws2, nblk2, None, db2)], C, accumulate=True)
+    dwr, dbr = dw0.to(BF).to(cuda), db0.to(BF).to(cuda)
+    K_.layernorm_bwd(dy.to(cuda), x.to(cuda), w.to(cuda), mean, rstd, dw=dwr, db=dbr, accumulate_wb=True)
+    assert torch.equal(dwb, dwr) and torch.equal(dbb, dbr)
+    assert rel_err(db2.float().cpu().numpy(), dy[:h].float().sum(0).numpy()) < 1e-2
 
 
 # ------------------------------------------------------------------------- attention

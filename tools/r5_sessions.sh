@@ -136,5 +136,25 @@ r5l)  # the tied lm_head's dW deferred and grouped with the blocks' (ABI v11 dev
 r5m)  # wide K = 768 plain products on the AGPR four-wave kernel (GVL_W4X=2) vs the persistent kernel
   for v in 1 2 1 2; do GVL_W4X=$v timeout -k 10 240 python -u tools/pp3_sweep.py > $O/sweep_w4x$v.log 2>&1; fatal $? sweep; echo "== GVL_W4X=$v"; grep -v amdgpu.ids $O/sweep_w4x$v.log; done
   ;;
+r5o)  # kernel trace (sequence) of the LM step
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/trace_lm.json 2> $O/trace_lm.err; fatal $? trace_lm
+  ;;
+r5n)  # kernel traces (sequence) of one graphed Q-Former / cross / linear step
+  for w in qformer cross; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace_$w -o $w -- \
+      python bench.py --workload $w --steps 2 --warmup 2 --no-cpu-baseline > $O/trace_$w.json 2> $O/trace_$w.err; fatal $? trace_$w
+  done
+  ;;
+r5p)  # LayerNorm weight grads deferred, one batched finalize per flush (ABI v12); LM trace
+  ktests kt "layernorm or grouped"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "bench_shape" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "full_size or accumulation" tests/test_gpu_parity_full.py
+  ktests dp "" tests/test_gpu_dp.py
+  ktests bnd "" tests/test_gpu_boundary.py
+  for r in 1 2; do for v in 1 0; do GVL_DEFER_LN=$v bench lm_ln${v}_$r lm; GVL_DEFER_LN=$v bench qf_ln${v}_$r qformer; done; done
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/trace_lm.json 2> $O/trace_lm.err; fatal $? trace_lm
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
