@@ -159,6 +159,21 @@ struct XSlabB<256, MN> {
 // waves of 128 x 128 (8 x 8 fragments = all 256 AGPRs, 0.25 reads per MFMA).
 // GR: a grouped launch (gvl_gemm_grouped): the problems differ in M, N, K and strides
 // (GemmP::Mb.. / gtile), read per tile.
+// Residual folded into the accumulators (GVL_W4X_FOLD, default 1; build-time A/B): for the
+// bias + residual epilogue (the LM's attn.c_proj / mlp.c_proj forward, x + yW^T + b with one
+// 256 x 192 tile per CU) the residual tile is read at the tile's start, before the prologue's
+// DMA and while no fragment registers are live (the K-loop has no registers to spare), and
+// becomes the accumulators' initial value (acc = residual + AB), so the epilogue stores
+// acc + bias with no operand read.  Round 4's form (half of the residual two K-steps ahead,
+// half in the epilogue) cost ~9.5 us per GEMM over the plain product at M = 16384; this one
+// takes 1.4 / 3.4 us of that back (attn.c_proj / mlp.c_proj forward: 33.1 vs 34.5, 79.7 vs
+// 83.1 us; profiles/r5/w4x_fold_r5q_r5r.txt) — the residual's 25 MB read, wherever it sits in
+// a one-tile-per-CU launch, is most of the rest.  Needs alpha == 1 (the planner sends no other
+// bias + residual GEMM here).
+#ifndef GVL_W4X_FOLD
+#define GVL_W4X_FOLD 1
+#endif
+
 template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR>
 GVL_DEV void gemm_w4x_body(const GemmP& p) {
   constexpr int NS = x_ns<BM>(), FM = BM / 32, FN = BN / 32;
@@ -242,6 +257,24 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
     EpiPre<FM, FN, EPI> pre;
     pre.load_bias(p, n0 + bcol, lane);
     const int aux_at = nks >= 2 ? nks - 2 : 0;
+    // (the planner sends only alpha == 1, >= 12 K-step bias + residual GEMMs here: gemm_w4x_plan)
+    constexpr bool FOLD = GVL_W4X_FOLD && EPI == EPI_BIAS_RES && !GR && !AMN;
+    // the residual tile, read before the prologue's DMA (no fragment registers live yet)
+    uint2 rx[FOLD ? FM : 1][FOLD ? FN : 1];
+    if constexpr (FOLD) {
+      // 8-B loads in the accumulator layout (the epilogue's 16-B store pattern + lane swaps
+      // measured no better here: profiles/r5/w4x_fold_r5q_r5r.txt)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t m = m0 + arow + 16 * i + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int64_t n = n0 + bcol + 16 * j + 4 * (lane >> 4);
+          rx[i][j] = (m < p.M && n < p.N) ? *reinterpret_cast<const uint2*>(res + m * p.ldr + n)
+                                          : make_uint2(0, 0);
+        }
+      }
+    }
 
 #define W4X_PIECE_A(t, step) \
   w4x_piece(ra, smem + ((step) % NS) * SLOT + ((t) * 4 + wave) * 1024, offa[t], (step) * sa_step)
@@ -261,7 +294,14 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (FOLD) {
+          const uint2 v = rx[i][j];
+          acc[i][j] = float4_t{lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y)};
+        } else {
+          acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+        }
+      }
     if constexpr (DB) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) bacc[k] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -295,7 +335,7 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
       wait_vm_steps<PER, NS - 3>(r_ < 0 ? 0 : (r_ < NS - 3 ? r_ : NS - 3));                    \
     }                                                                                          \
     __builtin_amdgcn_s_barrier();                                                              \
-    if (!(FULL) && !BMN && EpiKind<EPI>::AUX && (c) == aux_at)  /* BMN: it would spill */        \
+    if (!(FULL) && !BMN && EpiKind<EPI>::AUX && !FOLD && (c) == aux_at)  /* BMN: it would spill */ \
       pre.load_aux(p, m0 + arow, n0 + bcol, lane, 0, res), pre.pre0 = true;                   \
     const bool nx_ = FULL || (c) + 1 < nks, dm_ = FULL || (c) + NS - 1 < nks;                  \
     const char* sl_ = smem + (((c) + 1) % NS) * SLOT;                                          \
@@ -352,6 +392,11 @@ GVL_DEV void gemm_w4x_body(const GemmP& p) {
       GemmP q = p;
       q.M = M_, q.N = N_, q.ldc = ldc_, q.ldr = ldc_;
       gemm_epilogue16<FM, FN, EPI>(q, acc, m0 + arow, n0 + bcol, lane, alpha, pre, cout, res);
+    } else if constexpr (FOLD) {  // the residual is in acc: bias only
+      EpiPre<FM, FN, EPI_BIAS> pb;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) pb.b[j] = pre.b[j];
+      gemm_epilogue16<FM, FN, EPI_BIAS>(p, acc, m0 + arow, n0 + bcol, lane, alpha, pb, cout, nullptr);
     } else {
       gemm_epilogue16<FM, FN, EPI>(p, acc, m0 + arow, n0 + bcol, lane, alpha, pre, cout, res);
     }
@@ -423,6 +468,8 @@ bool gemm_w4x_plan(GemmP& p, int a_mn, int b_mn, bool force) {
   if ( p.c_f32 || p.K % KS != 0 || p.K < 2 * KS || p.N % 8 != 0 || p.ldc % 8 != 0 ||
       p.lda % 8 != 0 || p.ldb % 8 != 0 || (epi != EPI_PLAIN && epi != EPI_BIAS_RES))
     return false;
+  // the folded residual (GVL_W4X_FOLD) needs alpha == 1
+  if (GVL_W4X_FOLD && epi == EPI_BIAS_RES && (p.alpha != 1.f || p.alpha_ptr)) return false;
   (void)b_mn;
   // 256-row tiles where they (nearly) fill the chip, else 128-row tiles
   const int64_t cus = num_cus(), tn = (p.N + 192 - 1) / 192;

@@ -156,5 +156,20 @@ r5p)  # LayerNorm weight grads deferred, one batched finalize per flush (ABI v12
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace_lm -o lm -- \
     python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/trace_lm.json 2> $O/trace_lm.err; fatal $? trace_lm
   ;;
+r5q)  # LM N = 768 shapes at 16384 rows: model epilogue vs plain (w4x), both B layouts
+  for r in 1 2; do diag r$r 16384 narrow all; done
+  ;;
+r5r)  # residual folded into the AGPR accumulators at tile start (w4x bias + residual) vs libgvl_nofold.so
+  ktests kt "w4x or residual or tile128x192 or caption_dx"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "bench_shape" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for L in base nofold; do
+    LIB=$LIBDIR/libgvl.so; [ $L = nofold ] && LIB=$LIBDIR/libgvl_nofold.so
+    GVL_LIB=$LIB diag ${L}_$r 16384 narrow epi
+  done; done
+  for r in 1 2; do for L in base nofold; do
+    LIB=$LIBDIR/libgvl.so; [ $L = nofold ] && LIB=$LIBDIR/libgvl_nofold.so
+    GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
