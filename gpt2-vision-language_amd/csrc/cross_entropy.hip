@@ -15,6 +15,24 @@ namespace {
 #define GVL_CE_NT 512
 #endif
 constexpr int CE_NT = GVL_CE_NT;
+// cache policy A/B (build time): GVL_CE_LDNT=1 nontemporal logit loads, GVL_CE_STNT=1
+// nontemporal dlogits stores
+#ifndef GVL_CE_LDNT
+#define GVL_CE_LDNT 0
+#endif
+#ifndef GVL_CE_STNT
+#define GVL_CE_STNT 0
+#endif
+typedef uint32_t ce_u32x4 __attribute__((ext_vector_type(4)));
+GVL_DEV uint4 ce_load(const bf16_t* p) {
+  if constexpr (GVL_CE_LDNT)
+    return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const ce_u32x4*>(p)));
+  return *reinterpret_cast<const uint4*>(p);
+}
+GVL_DEV void ce_store(bf16_t* p, uint4 v) {
+  if constexpr (GVL_CE_STNT) __builtin_nontemporal_store(__builtin_bit_cast(ce_u32x4, v), reinterpret_cast<ce_u32x4*>(p));
+  else *reinterpret_cast<uint4*>(p) = v;
+}
 constexpr int CE_MAXC = 8192 / CE_NT;  // 16-B chunks per thread: V <= 65536
 constexpr float CE_L2E = 1.4426950408889634f;
 
@@ -66,7 +84,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
   for (int i = 0; i < CE_MAXC; ++i) {
     const int c = tid + i * CE_NT;
     if (c < nch) {
-      buf[i] = *reinterpret_cast<const uint4*>(src + (int64_t)c * 8);
+      buf[i] = ce_load(src + (int64_t)c * 8);
       if ((int64_t)c * 8 + 8 > V) buf[i] = mask_tail(buf[i], V - (int64_t)c * 8);
       const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
 #pragma unroll
@@ -107,7 +125,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
           if (base + 2 * k + 1 == tgt) b -= 1.f;
           o[k] = pack2(a, b);
         }
-        *reinterpret_cast<uint4*>(dst + base) = make_uint4(o[0], o[1], o[2], o[3]);
+        ce_store(dst + base, make_uint4(o[0], o[1], o[2], o[3]));
       }
     }
   }

@@ -171,5 +171,19 @@ r5r)  # residual folded into the AGPR accumulators at tile start (w4x bias + res
     GVL_LIB=$LIB bench lm_${L}_$r lm
   done; done
   ;;
+r5s)  # cross-entropy cache policy: nontemporal dlogits stores / logit loads (variant builds)
+  for r in 1 2; do for L in base cest celd ceboth; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ce_one.py > $O/ce_${L}_$r.log 2>&1; fatal $? ce
+    echo "$L $r: $(grep rows= $O/ce_${L}_$r.log | tr '\n' ' ')"
+  done; done
+  ;;
+r5t)  # cross-entropy nontemporal loads + stores (libgvl_ceboth.so) in the steps
+  for r in 1 2 3; do for L in base ceboth; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer
+    GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
