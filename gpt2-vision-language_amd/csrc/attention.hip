@@ -115,6 +115,24 @@ GVL_DEV short8_t frag_tr(const char* lds, int t, int s, int lane) {
   return r;
 }
 
+// Branch-free forms: rows past the end read row 0 (finite data) instead of being zero-filled.
+// Every use of such a row in attn_bwd_short_kernel is multiplied by a masked (exactly zero)
+// probability or score gradient, or not stored, so the results are unchanged; with no branch or
+// select on the loaded data hipcc issues the block's loads back to back and waits once, instead
+// of one round trip per conditional load (the prologue was six).
+GVL_DEV void load_rows_nb(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t R, int tid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    r[it] = *reinterpret_cast<const uint4*>(base + (row < R ? row : 0) * st + ch * 8);
+  }
+}
+GVL_DEV short8_t load_frag_global_nb(const bf16_t* rowptr0, int64_t st, int row, int s, int lane,
+                                     bool ok) {
+  return __builtin_bit_cast(
+      short8_t, *reinterpret_cast<const uint4*>(rowptr0 + (ok ? row : 0) * st + 32 * s + 8 * (lane >> 4)));
+}
+
 GVL_DEV short8_t load_frag_global(const bf16_t* rowptr, int s, int lane, bool ok) {
   if (!ok) return short8_t{0, 0, 0, 0, 0, 0, 0, 0};
   const uint4 u = *reinterpret_cast<const uint4*>(rowptr + 32 * s + 8 * (lane >> 4));
@@ -1042,42 +1060,45 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
   const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
   const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
-  {
-    uint4 r[2];
-    load_rows(r, qbase, p.q_st, 0, p.Tq, tid);
-    store_rows<false>(r, qs, tid);
-    load_rows(r, kbase, p.k_st, 0, p.Tk, tid);
-    store_rows<false>(r, ks, tid);
-    load_rows(r, vbase, p.v_st, 0, p.Tk, tid);
-    store_rows<false>(r, vs, tid);
-    load_rows(r, dobase, gg.do_st, 0, p.Tq, tid);
-    store_rows<false>(r, ds, tid);
-  }
-  // phase 1: this lane's query, its D (4 lanes x 16 dims of dO . O) and log-sum-exp
+  // every global operand of the block issued before the first wait (branch-free loads)
   const int ql = wave * 16 + (lane & 15);
   const bool qok = ql < p.Tq;
   const int64_t ridx = bh * p.Tq + ql;
-  float Dq = 0.f, lse2 = 0.f;
-  short8_t qf[2], df[2];
-  if (qok) {
-    const uint4* orow = reinterpret_cast<const uint4*>(obase + ql * p.o_st + 16 * Gl);
-    const uint4* drow = reinterpret_cast<const uint4*>(dobase + ql * gg.do_st + 16 * Gl);
+  const int qlc = qok ? ql : 0;
+  uint4 rq[2], rk[2], rv[2], rd[2], oa[2], da[2];
+  load_rows_nb(rq, qbase, p.q_st, p.Tq, tid);
+  load_rows_nb(rk, kbase, p.k_st, p.Tk, tid);
+  load_rows_nb(rv, vbase, p.v_st, p.Tk, tid);
+  load_rows_nb(rd, dobase, gg.do_st, p.Tq, tid);
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint4 a = orow[c], d = drow[c];
-      Dq += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
-            hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
-            lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
-    }
-    lse2 = p.lse[ridx] * LOG2E;
+  for (int c = 0; c < 2; ++c) {
+    oa[c] = reinterpret_cast<const uint4*>(obase + qlc * p.o_st + 16 * Gl)[c];
+    da[c] = reinterpret_cast<const uint4*>(dobase + qlc * gg.do_st + 16 * Gl)[c];
   }
-  Dq += __shfl_xor(Dq, 16, 64);
-  Dq += __shfl_xor(Dq, 32, 64);
+  const float lse_raw = p.lse[bh * p.Tq + qlc];
+  short8_t qf[2], df[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    qf[s2] = load_frag_global(qbase + ql * p.q_st, s2, lane, qok);
-    df[s2] = load_frag_global(dobase + ql * gg.do_st, s2, lane, qok);
+    qf[s2] = load_frag_global_nb(qbase, p.q_st, ql, s2, lane, qok);
+    df[s2] = load_frag_global_nb(dobase, gg.do_st, ql, s2, lane, qok);
   }
+  store_rows<false>(rq, qs, tid);
+  store_rows<false>(rk, ks, tid);
+  store_rows<false>(rv, vs, tid);
+  store_rows<false>(rd, ds, tid);
+  // phase 1: this lane's query, its D (4 lanes x 16 dims of dO . O) and log-sum-exp
+  float Dq = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint4 a = oa[c], d = da[c];
+    Dq += lo_bf(a.x) * lo_bf(d.x) + hi_bf(a.x) * hi_bf(d.x) + lo_bf(a.y) * lo_bf(d.y) +
+          hi_bf(a.y) * hi_bf(d.y) + lo_bf(a.z) * lo_bf(d.z) + hi_bf(a.z) * hi_bf(d.z) +
+          lo_bf(a.w) * lo_bf(d.w) + hi_bf(a.w) * hi_bf(d.w);
+  }
+  if (!qok) Dq = 0.f;
+  const float lse2 = qok ? lse_raw * LOG2E : 0.f;
+  Dq += __shfl_xor(Dq, 16, 64);
+  Dq += __shfl_xor(Dq, 32, 64);
   __syncthreads();
   float4_t sc[4], dp[4];
 #pragma unroll

@@ -185,5 +185,18 @@ r5t)  # cross-entropy nontemporal loads + stores (libgvl_ceboth.so) in the steps
     GVL_LIB=$LIB bench lm_${L}_$r lm
   done; done
   ;;
+r5u)  # short-sequence attention backward: all global loads issued before the first wait (vs libgvl_old.so)
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or linear or cross" tests/test_gpu_parity_bench.py
+  for r in 1 2 3; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep "B=128" $O/attn_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
