@@ -229,6 +229,7 @@ __global__ __launch_bounds__(256) void emb_pos_kernel(const bf16_t* __restrict__
 // 33 tokens are L2-normalised with F.normalize's max(||x||, 1e-12).
 constexpr int POOL_NT = 256;
 constexpr int POOL_MAXD = 4;  // D <= 1024
+constexpr int POOL_WIN = 8;   // pooling windows up to 8 patches (side 16: 4 x 2) take the unrolled path
 
 template <typename TIn>
 GVL_DEV float ld_in(const TIn* p);
@@ -254,23 +255,58 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
     c0 = (j * side) / 8;
     c1 = ((j + 1) * side + 7) / 8;
   }
-  const float inv_cnt = 1.f / (float)((r1 - r0) * (c1 - c0));
+  const int wc = c1 - c0, nwin = (r1 - r0) * wc;
+  const float inv_cnt = 1.f / (float)nwin;
   float ss = 0.f;
+  if (nwin <= POOL_WIN) {
+    // the window's loads unrolled with clamped indices (no branch between them), so every load of
+    // the block is in flight before the first add waits (a runtime-bounded loop issued one
+    // dependent load per iteration: 8 round trips per column at side 16)
+    float v[POOL_MAXD][POOL_WIN];
 #pragma unroll
-  for (int k = 0; k < POOL_MAXD; ++k) {
-    const int d = threadIdx.x + k * POOL_NT;
-    float a = 0.f;
-    if (d < D) {
-      if (o == 0) {
-        a = ld_in<TIn>(base + d);
-      } else {
-        for (int y = r0; y < r1; ++y)
-          for (int x = c0; x < c1; ++x) a += ld_in<TIn>(base + (1 + (int64_t)y * side + x) * D + d);
-        a *= inv_cnt;
+    for (int k = 0; k < POOL_MAXD; ++k) {
+      const int d = threadIdx.x + k * POOL_NT;
+      const int dc = d < D ? d : 0;
+#pragma unroll
+      for (int t = 0; t < POOL_WIN; ++t) {
+        const int tc = t < nwin ? t : 0;
+        const int y = r0 + tc / wc, x = c0 + tc % wc;
+        const int64_t row = o == 0 ? 0 : 1 + (int64_t)y * side + x;
+        v[k][t] = ld_in<TIn>(base + row * D + dc);
       }
     }
-    acc[k] = a;
-    ss += a * a;
+#pragma unroll
+    for (int k = 0; k < POOL_MAXD; ++k) {
+      const int d = threadIdx.x + k * POOL_NT;
+      float a = 0.f;
+      if (o == 0) {
+        a = v[k][0];
+      } else {
+#pragma unroll
+        for (int t = 0; t < POOL_WIN; ++t) a += t < nwin ? v[k][t] : 0.f;
+        a *= inv_cnt;
+      }
+      if (d >= D) a = 0.f;
+      acc[k] = a;
+      ss += a * a;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < POOL_MAXD; ++k) {
+      const int d = threadIdx.x + k * POOL_NT;
+      float a = 0.f;
+      if (d < D) {
+        if (o == 0) {
+          a = ld_in<TIn>(base + d);
+        } else {
+          for (int y = r0; y < r1; ++y)
+            for (int x = c0; x < c1; ++x) a += ld_in<TIn>(base + (1 + (int64_t)y * side + x) * D + d);
+          a *= inv_cnt;
+        }
+      }
+      acc[k] = a;
+      ss += a * a;
+    }
   }
   ss = block_sum<POOL_NT>(ss, red);
   const float scale = normalize ? 1.f / fmaxf(sqrtf(ss), 1e-12f) : 1.f;

@@ -1285,3 +1285,14 @@ def test_colsum_dropout_gate(cuda):
     assert rel_err(dy.float().cpu().numpy(), (t * x.float()).numpy()) < 8e-3
     want_g = (x.float() * y.float()).sum().item() * (1 - t * t)
     assert abs(acc.item() - want_g) / abs(want_g) < 1e-3
+    # 96 columns take the 8-wide kernels (round 5); 45 (and 37 x 45 elements) the scalar ones
+    x2, y2 = torch.randn(37, 45).to(BF), torch.randn(37, 45).to(BF)
+    d2 = K_.dropout_mask_apply(x2.to(cuda), p, seed)
+    keep2 = torch.from_numpy(keep_mask(seed, np.arange(x2.numel()), p).reshape(x2.shape))
+    want2 = torch.where(keep2, x2.float() / (1 - p), torch.zeros_like(x2.float()))
+    assert rel_err(d2.float().cpu().numpy(), want2.numpy()) < 8e-3
+    acc2 = torch.zeros(1, device=cuda)
+    dy2 = K_.gate_bwd(x2.to(cuda), y2.to(cuda), gate.to(cuda), acc2)
+    assert rel_err(dy2.float().cpu().numpy(), (t * x2.float()).numpy()) < 8e-3
+    want_g2 = (x2.float() * y2.float()).sum().item() * (1 - t * t)
+    assert abs(acc2.item() - want_g2) / abs(want_g2) < 1e-3

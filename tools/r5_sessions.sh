@@ -198,5 +198,13 @@ r5u)  # short-sequence attention backward: all global loads issued before the fi
     GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
   done; done
   ;;
+r5v)  # 8-wide dropout-apply / gate-backward, pooling window loads unrolled (vs libgvl_old.so)
+  ktests kt "colsum_dropout_gate or pool_clip or attention_short or gated"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross or linear" tests/test_gpu_parity_bench.py
+  for r in 1 2 3; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
