@@ -428,6 +428,22 @@ __global__ __launch_bounds__(RED_NT) void gate_finish_kernel(const float* __rest
   }
 }
 
+// gate_finish into a bf16 gradient (the sunk tanh-gate parameter's): g = bf16(g + bf16(dg)),
+// the same two roundings as autograd's bf16 gate grad added by AccumulateGrad
+__global__ __launch_bounds__(RED_NT) void gate_finish_bf16_kernel(const float* __restrict__ partial,
+                                                                  int nb, const bf16_t* __restrict__ gate,
+                                                                  bf16_t* __restrict__ g) {
+  __shared__ float red[RED_NT / 64];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += RED_NT) s += partial[i];
+  s = block_sum<RED_NT>(s, red);
+  if (threadIdx.x == 0) {
+    const float t = tanhf(bf2f(*gate));
+    const float dg = bf2f(f2bf(s * (1.f - t * t)));
+    *g = f2bf(bf2f(*g) + dg);
+  }
+}
+
 __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ in,
                                                           bf16_t* __restrict__ out, int64_t n,
                                                           int acc) {
@@ -624,9 +640,10 @@ extern "C" int64_t gvl_gate_bwd_workspace_size(int64_t n) {
   return (int64_t)red_blocks(n) * (int64_t)sizeof(float);
 }
 
-extern "C" int gvl_gate_bwd(const void* dx, const void* y, const void* gate, void* dy,
-                            float* gate_grad, int64_t n, void* workspace, gvl_stream_t stream) {
-  GVL_REQUIRE(dx && y && gate && dy && gate_grad && workspace, "gvl_gate_bwd: null buffer");
+static int gate_bwd_impl(const void* dx, const void* y, const void* gate, void* dy, float* gate_grad,
+                         void* gate_grad_bf16, int64_t n, void* workspace, gvl_stream_t stream) {
+  GVL_REQUIRE(dx && y && gate && dy && (gate_grad || gate_grad_bf16) && workspace,
+              "gvl_gate_bwd: null buffer");
   const int nb = red_blocks(n);
   hipStream_t s = gvl::as_stream(stream);
   const bool vec = n % 8 == 0 && gvl::aligned16(dx) && gvl::aligned16(y) && gvl::aligned16(dy);
@@ -640,11 +657,28 @@ extern "C" int gvl_gate_bwd(const void* dx, const void* y, const void* gate, voi
                        static_cast<const bf16_t*>(y), static_cast<const bf16_t*>(gate),
                        static_cast<bf16_t*>(dy), n, static_cast<float*>(workspace));
   GVL_LAUNCH_CHECK("gvl_gate_bwd");
-  hipLaunchKernelGGL(gate_finish_kernel, dim3(1), dim3(RED_NT), 0, s,
-                     static_cast<const float*>(workspace), vec ? nb8 : nb,
-                     static_cast<const bf16_t*>(gate), gate_grad);
+  if (gate_grad_bf16)
+    hipLaunchKernelGGL(gate_finish_bf16_kernel, dim3(1), dim3(RED_NT), 0, s,
+                       static_cast<const float*>(workspace), vec ? nb8 : nb,
+                       static_cast<const bf16_t*>(gate), static_cast<bf16_t*>(gate_grad_bf16));
+  else
+    hipLaunchKernelGGL(gate_finish_kernel, dim3(1), dim3(RED_NT), 0, s,
+                       static_cast<const float*>(workspace), vec ? nb8 : nb,
+                       static_cast<const bf16_t*>(gate), gate_grad);
   GVL_LAUNCH_CHECK("gvl_gate_bwd(finish)");
   return 0;
+}
+
+extern "C" int gvl_gate_bwd(const void* dx, const void* y, const void* gate, void* dy,
+                            float* gate_grad, int64_t n, void* workspace, gvl_stream_t stream) {
+  return gate_bwd_impl(dx, y, gate, dy, gate_grad, nullptr, n, workspace, stream);
+}
+
+extern "C" int gvl_gate_bwd_acc_bf16(const void* dx, const void* y, const void* gate, void* dy,
+                                     void* gate_grad, int64_t n, void* workspace,
+                                     gvl_stream_t stream) {
+  GVL_REQUIRE(gate_grad != nullptr, "gvl_gate_bwd_acc_bf16: null gate_grad");
+  return gate_bwd_impl(dx, y, gate, dy, nullptr, gate_grad, n, workspace, stream);
 }
 
 extern "C" int gvl_f32_to_bf16(const float* in, void* out, int64_t n, int32_t accumulate,

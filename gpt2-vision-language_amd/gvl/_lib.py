@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 12  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 13  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32
@@ -123,6 +123,7 @@ SIGNATURES = {
     "gvl_dropout_mask_apply": (C.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_u64, c_vp,
                                          c_vp]),
     "gvl_gate_bwd": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "gvl_gate_bwd_acc_bf16": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "gvl_gate_bwd_workspace_size": (c_i64, [c_i64]),
     "gvl_f32_to_bf16": (C.c_int, [c_vp, c_vp, c_i64, c_i32, c_vp]),
 }

@@ -134,6 +134,9 @@ DEFER_LMHEAD = os.environ.get("GVL_DEFER_LMHEAD", "1") != "0"
 # partials in a workspace and the flush reduces all of them in one launch
 # (gvl_layernorm_bwd_finalize_batched) instead of one finalize launch per LayerNorm
 DEFER_LN = os.environ.get("GVL_DEFER_LN", "1") != "0"
+# The cross-att tanh gate's gradient added into its bf16 grad by the gate kernel itself (ABI v13)
+# instead of an fp32 zero-fill + kernel + cast + autograd add per block (GVL_GATE_SINK=0: A/B)
+GATE_SINK = os.environ.get("GVL_GATE_SINK", "1") != "0"
 # Grouped flush (gvl_gemm_grouped) of the queued weight gradients of one stream over <= 8192
 # tokens: 2 (default) up to 48 problems (the cross-att decoder's 12 blocks' flush: +1.9 % on its
 # step, profiles/r4/grouped48_r4g48.txt), 1 up to 16 (the Q-Former bridge's), 0 off.  The LM's
@@ -878,7 +881,7 @@ class CrossAttnFn(torch.autograd.Function):
                          c_w, c_b, gate, n_head)
         if any(ctx.needs_input_grad):
             ctx.z2, ctx.kv_w = z2, kv_w
-            ctx.params = (None, None, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b)
+            ctx.params = (None, None, ln_w, ln_b, q_w, q_b, kv_w, kv_b, c_w, c_b, gate)
             ctx.idx = (0, 2, 3, 4, 5, 8, 9, 10)
         return out
 
@@ -923,10 +926,15 @@ def _xattn_bwd(ctx, dout, dkv, g):
     ix, iln_w, iln_b, iq_w, iq_b, ic_w, ic_b, igate = ctx.idx
     P = ctx.params
     d2 = dout.reshape(B * T, C).to(BF16).contiguous()
-    gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
-    dbr = K.gate_bwd(d2, ybr, gate, gacc)
-    if _need(ctx, igate):
-        g[igate] = gacc.to(gate.dtype).view_as(gate)
+    gsink = _sink(P[igate], ctx) if _need(ctx, igate) and GATE_SINK else None
+    if gsink is not None:  # added into the gate's bf16 grad in the finish kernel
+        dbr = K.gate_bwd(d2, ybr, gate, grad_bf16=gsink)
+        _ready(P[igate])
+    else:
+        gacc = torch.zeros(1, dtype=torch.float32, device=d2.device)
+        dbr = K.gate_bwd(d2, ybr, gate, gacc)
+        if _need(ctx, igate):
+            g[igate] = gacc.to(gate.dtype).view_as(gate)
     g[ic_w] = _wgrad(ctx, ic_w, P[ic_w], dbr, o.view(B * T, C), defer=True)
     g[ic_b] = _bgrad(ctx, ic_b, P[ic_b], dbr, defer=True)
     do = K.linear_dx(dbr, c_w).view(B, T, C)
@@ -1020,7 +1028,7 @@ class CrossAttnKVFn(torch.autograd.Function):
         out = _xattn_fwd(ctx, x, kv, 2 * C * layer, ln_w, ln_b, q_w, q_b, c_w, c_b, gate, n_head)
         if any(ctx.needs_input_grad):
             ctx.slab = slab
-            ctx.params = (None, None, None, None, ln_w, ln_b, q_w, q_b, c_w, c_b)
+            ctx.params = (None, None, None, None, ln_w, ln_b, q_w, q_b, c_w, c_b, gate)
             ctx.idx = (0, 4, 5, 6, 7, 8, 9, 10)
         return out
 

@@ -690,11 +690,21 @@ def dropout_mask_apply(x2, p, seed, out=None, seed_ptr=None):
     return out
 
 
-def gate_bwd(dx, y, gate, gate_grad_f32):
+def gate_bwd(dx, y, gate, gate_grad_f32=None, grad_bf16=None):
+    """dy = tanh(gate) * dx; the gate gradient (1 - tanh^2) * sum(dx * y) added into
+    gate_grad_f32 (fp32 scalar) or, with grad_bf16, into that bf16 scalar with autograd's
+    roundings (ABI v13)."""
     n = dx.numel()
     dy = torch.empty_like(dx)
     ws = torch.empty(max(_L().gvl_gate_bwd_workspace_size(n), 4) // 4, dtype=F32,
                      device=dx.device)
+    if grad_bf16 is not None:
+        if grad_bf16.dtype != BF16 or grad_bf16.numel() != 1:
+            raise TypeError("gvl.gate_bwd: grad_bf16 must be a bf16 scalar")
+        _lib.check(_L().gvl_gate_bwd_acc_bf16(dx.data_ptr(), y.data_ptr(), gate.data_ptr(),
+                                              dy.data_ptr(), grad_bf16.data_ptr(), n, ws.data_ptr(),
+                                              _stream()), "gvl_gate_bwd_acc_bf16")
+        return dy
     _lib.check(_L().gvl_gate_bwd(dx.data_ptr(), y.data_ptr(), gate.data_ptr(), dy.data_ptr(),
                                  gate_grad_f32.data_ptr(), n, ws.data_ptr(), _stream()),
                "gvl_gate_bwd")

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 12
+#define GVL_ABI_VERSION 13
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -366,6 +366,11 @@ int gvl_dropout_mask_apply(const void* in, int64_t ld_in, void* out, int64_t ld_
 int gvl_gate_bwd(const void* dx, const void* y, const void* gate, void* dy, float* gate_grad,
                  int64_t n, void* workspace, gvl_stream_t stream);
 int64_t gvl_gate_bwd_workspace_size(int64_t n);
+/* ABI v13: as gvl_gate_bwd, the gate gradient added into the bf16 scalar gate_grad (the gate
+ * parameter's own .grad): gate_grad = bf16(gate_grad + bf16(dgate)), the roundings of
+ * autograd's AccumulateGrad on a bf16 parameter — no fp32 scalar, zero-fill or conversion. */
+int gvl_gate_bwd_acc_bf16(const void* dx, const void* y, const void* gate, void* dy,
+                          void* gate_grad, int64_t n, void* workspace, gvl_stream_t stream);
 /* fp32 -> bf16 conversion with optional accumulate into the bf16 destination. */
 int gvl_f32_to_bf16(const float* in, void* out, int64_t n, int32_t accumulate,
                     gvl_stream_t stream);

@@ -1296,3 +1296,11 @@ def test_colsum_dropout_gate(cuda):
     assert rel_err(dy2.float().cpu().numpy(), (t * x2.float()).numpy()) < 8e-3
     want_g2 = (x2.float() * y2.float()).sum().item() * (1 - t * t)
     assert abs(acc2.item() - want_g2) / abs(want_g2) < 1e-3
+    # ABI v13: the gate gradient added into a bf16 scalar grad with autograd's roundings
+    for xx, yy, wg in ((x, y, want_g), (x2, y2, want_g2)):
+        gb = torch.tensor(0.75).to(BF).to(cuda)
+        dyb = K_.gate_bwd(xx.to(cuda), yy.to(cuda), gate.to(cuda), grad_bf16=gb)
+        assert torch.equal(dyb.cpu(), K_.gate_bwd(xx.to(cuda), yy.to(cuda), gate.to(cuda),
+                                                  torch.zeros(1, device=cuda)).cpu())
+        want_b = (torch.tensor(0.75).to(BF).float() + torch.tensor(wg).to(BF).float()).to(BF)
+        assert abs(gb.float().item() - want_b.float().item()) <= 2 ** -7 * abs(want_b.float().item())

@@ -55,7 +55,10 @@ def test_traffic_table_from_counter_csvs(tmp_path):
 def test_committed_traffic_covers_bench_dominant_kernels():
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         t = json.load(f)["workloads"]
-    # the dominant GEMMs of the round-4 bench lines (profiles/r4/bench_r4v.json), with MFMA busy
-    # and the exact MFMA-rate fraction
-    for wl, name in (("lm", "gemm_w4x_kernel<256, 256, true, true, 6, false>"), ("qf", "gemm_w4d_kernel<false, 2>")):
+    # the dominant GEMMs of the latest committed closing bench line (profiles/r5/bench_r5fin.json:
+    # the LM line's and the Q-Former line's roofline kernels), with MFMA busy and the exact
+    # MFMA-rate fraction
+    with open(os.path.join(ROOT, "profiles", "r5", "bench_r5fin.json")) as f:
+        b = json.load(f)
+    for wl, name in (("lm", b["roofline"]["kernel"]), ("qf", b["caption_qformer"]["roofline"]["kernel"])):
         assert t[wl][name]["hbm_bytes"] > 0 and 0 < t[wl][name]["mfma_rate_frac"] < 1

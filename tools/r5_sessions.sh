@@ -206,5 +206,12 @@ r5v)  # 8-wide dropout-apply / gate-backward, pooling window loads unrolled (vs 
     GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
   done; done
   ;;
+r5w)  # cross-att gate gradient accumulated into its bf16 grad by the gate kernel (ABI v13) vs GVL_GATE_SINK=0
+  ktests kt "colsum_dropout_gate or gated"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "cross" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "cross" tests/test_gpu_parity_full.py
+  ktests capi "" tests/test_capi.py
+  for r in 1 2 3; do for v in 1 0; do GVL_GATE_SINK=$v bench cross_g${v}_$r cross; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
