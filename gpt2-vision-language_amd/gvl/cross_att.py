@@ -160,6 +160,9 @@ class GPT(nn.Module):
             for p in blk.xattn.parameters():
                 p.requires_grad = True
             blk.cross_gate.requires_grad = True
+            # consecutive arena slots for the stacked kv_proj GEMM (gvl.optim, Fn._stacked)
+            blk.xattn.kv_proj.weight._gvl_stack_key = "xattn.kv_proj.weight"
+            blk.xattn.kv_proj.bias._gvl_stack_key = "xattn.kv_proj.bias"
 
     def forward(self, idx, z=None, targets=None, target_mask=None):
         B, T = idx.size()

@@ -979,6 +979,20 @@ class KVGradSlab:
         return buf
 
 
+def _stacked(ts):
+    """torch.cat(ts, 0) — or, when the tensors already sit back to back in one storage (the gvl
+    AdamW arena places parameters tagged with one `_gvl_stack_key` consecutively), a view of
+    that storage with no copy."""
+    t0 = ts[0]
+    n, es = t0.numel(), t0.element_size()
+    if all(t.is_contiguous() and t.dtype == t0.dtype and t.shape == t0.shape and
+           t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr() and
+           t.data_ptr() == t0.data_ptr() + i * n * es for i, t in enumerate(ts)):
+        return t0.as_strided((len(ts) * t0.shape[0],) + tuple(t0.shape[1:]),
+                             (t0.stride(0),) + tuple(t0.stride()[1:]))
+    return torch.cat(ts, 0)
+
+
 class CrossKVFn(torch.autograd.Function):
     """kv_proj of ALL cross-attention blocks (gpt2_cross-att/model.py:49-50 in each Block)
     over the same projected CLIP tokens as one GEMM against the stacked weights
@@ -991,8 +1005,8 @@ class CrossKVFn(torch.autograd.Function):
         L = len(wb) // 2
         B, S, C = z.shape
         z2 = z.reshape(B * S, C).to(BF16).contiguous()
-        w_all = torch.cat(wb[0::2], 0)
-        kv = K.linear(z2, w_all, torch.cat(wb[1::2], 0))
+        w_all = _stacked(wb[0::2])
+        kv = K.linear(z2, w_all, _stacked(wb[1::2]))
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(z2, w_all)
             ctx.cfg = (B, S, C, L)

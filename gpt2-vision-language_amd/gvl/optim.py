@@ -61,9 +61,25 @@ class AdamW(torch.optim.Optimizer):
         total = 0
         for g in self.param_groups:
             start = total
+            # parameters tagged with the same `_gvl_stack_key` (the cross-att blocks' kv_proj
+            # weights / biases, which gvl.functional.CrossKVFn multiplies as ONE stacked matrix)
+            # get consecutive arena slots at the first one's place, so the stack is a view of the
+            # arena instead of a per-step torch.cat; the param_groups order (and so the optimizer
+            # state_dict's parameter indices) is unchanged
+            stacks = {}
             for p in g["params"]:
-                offs.append(total)
-                total += _pad(p.numel())
+                k = getattr(p, "_gvl_stack_key", None)
+                if k is not None:
+                    stacks.setdefault(k, []).append(p)
+            placed = {}
+            for p in g["params"]:
+                if id(p) in placed:
+                    continue
+                k = getattr(p, "_gvl_stack_key", None)
+                for q in (stacks[k] if k is not None else [p]):
+                    placed[id(q)] = total
+                    total += _pad(q.numel())
+            offs.extend(placed[id(p)] for p in g["params"])
             seg.append((start, total))
         total = max(total, _ALIGN)
         sdt = F32 if self.master_weights else BF16

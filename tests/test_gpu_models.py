@@ -113,6 +113,12 @@ def test_three_adamw_steps(cuda, golden, meta, kind):
     params = dict(m.named_parameters())
     for n in named_trainable(kind, meta):
         check_summary(fx, "step3:" + n, params[n].float(), 8e-2)
+    if kind == "cross":  # the arena keeps the blocks' kv_proj back to back: a view, no cat
+        import gvl.functional as Fn
+        for attr in ("weight", "bias"):
+            ts = [getattr(blk.xattn.kv_proj, attr) for blk in m.transformer.h]
+            st = Fn._stacked(ts)
+            assert st.data_ptr() == ts[0].data_ptr() and torch.equal(st, torch.cat(ts, 0))
 
 
 def test_grad_accumulation_equivalence(cuda, meta, golden):

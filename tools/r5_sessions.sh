@@ -213,5 +213,13 @@ r5w)  # cross-att gate gradient accumulated into its bf16 grad by the gate kerne
   ktests capi "" tests/test_capi.py
   for r in 1 2 3; do for v in 1 0; do GVL_GATE_SINK=$v bench cross_g${v}_$r cross; done; done
   ;;
+r5x)  # cross-att kv_proj stacked in the optimizer arena (view instead of torch.cat per step)
+  ktests models "cross" tests/test_gpu_models.py
+  ktests dp "" tests/test_gpu_dp.py
+  ktests bnd "" tests/test_gpu_boundary.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "cross" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "cross" tests/test_gpu_parity_full.py
+  for r in 1 2 3; do bench cross_$r cross; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
