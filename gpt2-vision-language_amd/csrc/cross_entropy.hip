@@ -138,6 +138,9 @@ __global__ __launch_bounds__(1024) void ce_finalize_kernel(const float* __restri
                                                            float* __restrict__ out) {
   __shared__ float red[16];
   float s = 0.f, n = 0.f;
+  // unrolled: the loads of several rows in flight per thread (a rolled loop waited for each
+  // row's target and loss in turn: 17 us for the LM's 16384 rows)
+#pragma unroll 8
   for (int64_t r = threadIdx.x; r < rows; r += 1024) {
     const bool mk = (mask == nullptr || mask[r] != 0);
     const bool valid = (targets[r] != -100) && mk;

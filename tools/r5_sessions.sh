@@ -221,5 +221,34 @@ r5x)  # cross-att kv_proj stacked in the optimizer arena (view instead of torch.
   GVL_MARGINS_DIR=$O/parity_margins ktests full "cross" tests/test_gpu_parity_full.py
   for r in 1 2 3; do bench cross_$r cross; done
   ;;
+r5y)  # CE finalize loads unrolled; kernel traces (sequence) of all four steps at head
+  ktests kt "cross_entropy or lm_head"
+  for w in qformer cross linear; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace_$w -o $w -- \
+      python bench.py --workload $w --steps 2 --warmup 2 --no-cpu-baseline > $O/trace_$w.json 2> $O/trace_$w.err; fatal $? trace_$w
+  done
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/trace_lm.json 2> $O/trace_lm.err; fatal $? trace_lm
+  ;;
+r5z)  # software-pipelined attention forward (S(kt+1) || exp(kt)) vs attn_fwd_dma_kernel (GVL_ATTN_FWD_PIPE=0); CE finalize
+  ktests kt "attention or attn or cross_entropy"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "lm" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in 1 0; do
+    GVL_ATTN_FWD_PIPE=$v timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_p${v}_$r.log 2>&1; fatal $? attn
+    echo "attn pipe=$v $r"; grep "B=16" $O/attn_p${v}_$r.log
+  done; done
+  for r in 1 2; do for v in 1 0; do GVL_ATTN_FWD_PIPE=$v bench lm_p${v}_$r lm; done; done
+  ;;
+r5z2)  # pipelined forward: 3-slot ring (default build) vs 4-slot (libgvl_p4.so), picked G vs G = 1
+  ktests kt "attention or attn"
+  GVL_ATTN_FWD_PIPE=2 ktests kt2 "attention or attn"
+  GVL_LIB=$LIBDIR/libgvl_p4.so GVL_ATTN_FWD_PIPE=2 ktests kt3 "attention or attn"
+  for r in 1 2; do for L in base p4; do for v in 0 1 2; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB GVL_ATTN_FWD_PIPE=$v timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_${v}_$r.log 2>&1; fatal $? attn
+    echo "attn $L pipe=$v $r: $(grep B=16 $O/attn_${L}_${v}_$r.log)"
+  done; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
