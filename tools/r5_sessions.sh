@@ -250,5 +250,13 @@ r5z2)  # pipelined forward: 3-slot ring (default build) vs 4-slot (libgvl_p4.so)
     echo "attn $L pipe=$v $r: $(grep B=16 $O/attn_${L}_${v}_$r.log)"
   done; done; done
   ;;
+r5y2)  # CE finalize: branch-free row loads, mask presence as a template argument
+  ktests kt "cross_entropy or lm_head"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm or cross or linear" tests/test_gpu_parity_bench.py
+  ktests models "forward_loss or masked" tests/test_gpu_models.py
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  f=$(find $O/prof_lm -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lm_table.txt; grep -E "ce_|emb_" $O/lm_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
