@@ -125,6 +125,9 @@ __global__ __launch_bounds__(EMB_TILE) void emb_rank_kernel(const uint32_t* __re
   if (rank < n) out[rank] = key;
 }
 
+// Load order: the run head's key and its predecessor together; then the wte row, the first dout
+// row and the NEXT key together (and each further dout row with the key after it), so a run of
+// one token — most of them — costs three dependent round trips instead of five.
 __global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict__ keys, int n,
                                                        int64_t base, const bf16_t* __restrict__ dout,
                                                        bf16_t* __restrict__ dwte, int64_t T,
@@ -132,42 +135,57 @@ __global__ __launch_bounds__(256) void emb_seg_kernel(const uint32_t* __restrict
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const uint32_t key = keys[i];
+  const uint32_t prev = keys[i > 0 ? i - 1 : i];
   const uint32_t id = key >> 14;
   if (id == EMB_BAD_ID) return;
-  if (i > 0 && (keys[i - 1] >> 14) == id) return;  // not the head of its run
+  if (i > 0 && (prev >> 14) == id) return;  // not the head of its run
   const int lane = threadIdx.x & 63;
+  bf16_t* w = dwte + (int64_t)id * C;
+  uint4 wu[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = lane * 8 + h * 512;
+    if (c < C) wu[h] = *reinterpret_cast<const uint4*>(w + c);
+  }
   float acc[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
-  for (int j = i; j < n; ++j) {
-    const uint32_t kj = keys[j];
-    if ((kj >> 14) != id) break;
+  uint32_t kj = key;
+  for (int j = i;;) {
     const int64_t r = base + (int64_t)(kj & 0x3FFFu);
     const bf16_t* g = dout + ((r / T) * S + off + r % T) * (int64_t)C;
+    uint4 u[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane * 8 + h * 512;
+      if (c < C) u[h] = *reinterpret_cast<const uint4*>(g + c);
+    }
+    const uint32_t kn = j + 1 < n ? keys[j + 1] : 0xFFFFFFFFu;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = lane * 8 + h * 512;
       if (c < C) {
-        const uint4 u = *reinterpret_cast<const uint4*>(g + c);
-        acc[h][0] += lo_bf(u.x); acc[h][1] += hi_bf(u.x); acc[h][2] += lo_bf(u.y);
-        acc[h][3] += hi_bf(u.y); acc[h][4] += lo_bf(u.z); acc[h][5] += hi_bf(u.z);
-        acc[h][6] += lo_bf(u.w); acc[h][7] += hi_bf(u.w);
+        acc[h][0] += lo_bf(u[h].x); acc[h][1] += hi_bf(u[h].x); acc[h][2] += lo_bf(u[h].y);
+        acc[h][3] += hi_bf(u[h].y); acc[h][4] += lo_bf(u[h].z); acc[h][5] += hi_bf(u[h].z);
+        acc[h][6] += lo_bf(u[h].w); acc[h][7] += hi_bf(u[h].w);
       }
     }
+    if ((kn >> 14) != id) break;
+    kj = kn;
+    ++j;
   }
-  bf16_t* w = dwte + (int64_t)id * C;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int c = lane * 8 + h * 512;
     if (c < C) {
-      const uint4 u = *reinterpret_cast<const uint4*>(w + c);
+      const uint4 uw = wu[h];
       uint4 o;
-      o.x = pack2(lo_bf(u.x) + acc[h][0], hi_bf(u.x) + acc[h][1]);
-      o.y = pack2(lo_bf(u.y) + acc[h][2], hi_bf(u.y) + acc[h][3]);
-      o.z = pack2(lo_bf(u.z) + acc[h][4], hi_bf(u.z) + acc[h][5]);
-      o.w = pack2(lo_bf(u.w) + acc[h][6], hi_bf(u.w) + acc[h][7]);
+      o.x = pack2(lo_bf(uw.x) + acc[h][0], hi_bf(uw.x) + acc[h][1]);
+      o.y = pack2(lo_bf(uw.y) + acc[h][2], hi_bf(uw.y) + acc[h][3]);
+      o.z = pack2(lo_bf(uw.z) + acc[h][4], hi_bf(uw.z) + acc[h][5]);
+      o.w = pack2(lo_bf(uw.w) + acc[h][6], hi_bf(uw.w) + acc[h][7]);
       *reinterpret_cast<uint4*>(w + c) = o;
     }
   }

@@ -258,5 +258,22 @@ r5y2)  # CE finalize: branch-free row loads, mask presence as a template argumen
     python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
   f=$(find $O/prof_lm -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lm_table.txt; grep -E "ce_|emb_" $O/lm_table.txt
   ;;
+r5ln)  # persistent LayerNorm forward (next row's loads before this row's stores) vs the one-shot grid
+  for L in p512 p1024 p2048; do GVL_LIB=$LIBDIR/libgvl_$L.so ktests kt_$L "layernorm"; done
+  for r in 1 2; do for L in base p512 p1024 p2048; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ln_one.py > $O/ln_${L}_$r.log 2>&1; fatal $? ln
+    echo "$L $r"; grep ln_fwd $O/ln_${L}_$r.log
+  done; done
+  ;;
+r5e2)  # persistent LayerNorm forward (default), embedding backward run-head loads overlapped: tests + LM / Q-Former steps + LM kernel table
+  ktests kt "layernorm or embedding or embed"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "lm or accumulation" tests/test_gpu_parity_full.py
+  for r in 1 2; do bench lm_$r lm; bench qf_$r qformer; done
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  f=$(find $O/prof_lm -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lm_table.txt; grep -E "ln_|emb_" $O/lm_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
