@@ -433,6 +433,17 @@ GVL_DEV void lds_wait8(short8_t (&a)[4], short8_t (&b)[4]) {
                : "memory");
 }
 
+// Mark register fragments loaded at kernel entry as landed HERE, after the ring's first DMA
+// instructions are issued: the asm takes them as inputs, so hipcc waits for their loads right
+// before it (counting the younger DMAs), and its outputs are what the loop uses, so no wait is
+// placed at their first use inside the loop (hipcc's count there drained the whole ring).  The
+// fragment loads and the first tiles' DMAs are then one round trip, not two in a row.
+template <int G>
+GVL_DEV void frags_landed(short8_t (&a)[G][2], short8_t (&b)[G][2]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" : "+v"(a[g][0]), "+v"(a[g][1]), "+v"(b[g][0]), "+v"(b[g][1]));
+}
+
 // Issue the lse and D float4 of one fragment row (ds_read_b128 at a and a + 256) without waiting;
 // lds_wait_pair<N> waits until at most N of this wave's LDS operations are in flight, with the
 // pair threaded through so no use is scheduled above the wait.  Early-clobber: a result must not
@@ -481,9 +492,6 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
       vf[g][s2] = load_frag_global(vbase + key[g] * p.v_st, s2, lane, kok[g]);
     }
   }
-  // K / V fragments landed before the ring's first DMA (else hipcc drains the ring at the loop entry)
-#pragma unroll
-  for (int g = 0; g < G; ++g) asm volatile("" ::"v"(kf[g][0]), "v"(kf[g][1]), "v"(vf[g][0]), "v"(vf[g][1]));
   const int qt_first = p.causal ? (int)(kblk0 / KT) : 0;
   const int nqt = (int)((p.Tq + KT - 1) / KT);
   const int nq = nqt - qt_first;
@@ -530,9 +538,15 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
     else if (wave < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   };
+  // the K / V fragments' loads and the first DMAs in flight together (the dropout instance
+  // keeps them apart: the extra live range spills it)
+  if constexpr (DROP) frags_landed<G>(kf, vf);
   if (nq > 0) {
     issue(qt_first, 0);
     if (nq > 1) issue(qt_first + 1, 1);
+  }
+  if constexpr (!DROP) frags_landed<G>(kf, vf);
+  if (nq > 0) {
     wait_tiles(nq > 1 ? 1 : 0);
     gvl_ring::barrier_lds();
   }
@@ -693,33 +707,18 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
   for (int g = 0; g < G; ++g) {
     q[g] = qblk0 + wave * 16 * G + g * 16 + (lane & 15);
     qok[g] = q[g] < p.Tq;
+    // branch-free (rows past Tq read row 0; their dQ is never stored and a query row's dQ
+    // depends on that row alone), so hipcc issues every prologue load back to back: the
+    // conditional forms cost four dependent round trips before the first DMA
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      qf[g][s2] = load_frag_global(qbase + q[g] * p.q_st, s2, lane, qok[g]);
-      df[g][s2] = load_frag_global(dobase + q[g] * gg.do_st, s2, lane, qok[g]);
+      qf[g][s2] = load_frag_global_nb(qbase, p.q_st, (int)q[g], s2, lane, qok[g]);
+      df[g][s2] = load_frag_global_nb(dobase, gg.do_st, (int)q[g], s2, lane, qok[g]);
     }
     const int64_t ridx = (b * p.H + h) * p.Tq + q[g];
-    lse2[g] = qok[g] ? p.lse[ridx] * LOG2E : 0.f;
+    const float lraw = p.lse[qok[g] ? ridx : (b * p.H + h) * p.Tq];
+    lse2[g] = qok[g] ? lraw * LOG2E : 0.f;
     drow[g] = (uint64_t)ridx * (uint64_t)p.Tk;
-  }
-  {  // D = rowsum(dO * O): this lane's 16 dims (8 at 32 s2 + 8 Gl, s2 = 0, 1), then the row's 4 lanes
-    const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float sd = 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const short8_t of = load_frag_global(obase + q[g] * p.o_st, s2, lane, qok[g]);
-        const uint4 ou = __builtin_bit_cast(uint4, of), du = __builtin_bit_cast(uint4, df[g][s2]);
-        const uint32_t ow[4] = {ou.x, ou.y, ou.z, ou.w}, dw[4] = {du.x, du.y, du.z, du.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sd += lo_bf(ow[k]) * lo_bf(dw[k]) + hi_bf(ow[k]) * hi_bf(dw[k]);
-      }
-      sd += __shfl_xor(sd, 16, 64);
-      sd += __shfl_xor(sd, 32, 64);
-      Dq[g] = qok[g] ? sd : 0.f;
-      if (qok[g] && Gl == 0) gg.Dws[(b * p.H + h) * p.Tq + q[g]] = sd;
-    }
   }
   int64_t kend = p.Tk;
   if (p.causal) {
@@ -752,6 +751,29 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
   if (nkt > 0) {
     issue(0, 0);
     if (nkt > 1) issue(1, 1);
+  }
+  {  // (after the first DMAs are issued: O / dO land under them) D = rowsum(dO * O): this lane's 16 dims (8 at 32 s2 + 8 Gl, s2 = 0, 1), then the row's 4 lanes
+    const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float sd = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const short8_t of = load_frag_global_nb(obase, p.o_st, (int)q[g], s2, lane, qok[g]);
+        const uint4 ou = __builtin_bit_cast(uint4, of), du = __builtin_bit_cast(uint4, df[g][s2]);
+        const uint32_t ow[4] = {ou.x, ou.y, ou.z, ou.w}, dw[4] = {du.x, du.y, du.z, du.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sd += lo_bf(ow[k]) * lo_bf(dw[k]) + hi_bf(ow[k]) * hi_bf(dw[k]);
+      }
+      sd += __shfl_xor(sd, 16, 64);
+      sd += __shfl_xor(sd, 32, 64);
+      Dq[g] = qok[g] ? sd : 0.f;
+    }
+  }
+  frags_landed<G>(qf, df);
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" : "+v"(lse2[g]));
+  if (nkt > 0) {
     if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gvl_ring::barrier_lds();
@@ -836,6 +858,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (!qok[g]) continue;
+    if (Gl == 0) gg.Dws[(b * p.H + h) * p.Tq + q[g]] = Dq[g];  // read by the dK/dV kernel
     bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + q[g] * gg.dq_st;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -878,10 +901,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
     qf[g][0] = load_frag_global(qbase + q[g] * p.q_st, 0, lane, qok[g]);
     qf[g][1] = load_frag_global(qbase + q[g] * p.q_st, 1, lane, qok[g]);
   }
-  // the Q fragments land before the first DMA is issued: waited for at their first use, they
-  // would make hipcc drain the whole prefetched ring (vmcnt(0)) at the loop entry
-#pragma unroll
-  for (int g = 0; g < G; ++g) asm volatile("" ::"v"(qf[g][0]), "v"(qf[g][1]));
   int64_t kend = p.Tk;
   if (p.causal) {
     const int64_t lim = qblk0 + QT;
@@ -920,6 +939,10 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
   if (nkt > 0) {
     issue(0, 0);
     if (nkt > 1) issue(1, 1);
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" : "+v"(qf[g][0]), "+v"(qf[g][1]));  // (frags_landed)
+  if (nkt > 0) {
     if (nkt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gvl_ring::barrier_lds();

@@ -275,5 +275,19 @@ r5e2)  # persistent LayerNorm forward (default), embedding backward run-head loa
     python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
   f=$(find $O/prof_lm -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lm_table.txt; grep -E "ln_|emb_" $O/lm_table.txt
   ;;
+r5aq)  # attention prologues: fragment loads + first DMAs in one round trip, branch-free dQ prologue (vs libgvl_old.so)
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2 3; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r: $(grep 'B=16 ' $O/attn_${L}_$r.log)"; grep "B=128 H=12 Tq=32 Tk=257" $O/attn_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB bench lm_${L}_$r lm; GVL_LIB=$LIB bench qf_${L}_$r qformer
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
