@@ -752,7 +752,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     issue(0, 0);
     if (nkt > 1) issue(1, 1);
   }
-  {  // (after the first DMAs are issued: O / dO land under them) D = rowsum(dO * O): this lane's 16 dims (8 at 32 s2 + 8 Gl, s2 = 0, 1), then the row's 4 lanes
+  // D = rowsum(dO * O), after the first DMAs are issued (O / dO land under them): this lane's
+  // 16 dims (8 at 32 s2 + 8 Gl, s2 = 0, 1), then the row's 4 lanes
+  {
     const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
