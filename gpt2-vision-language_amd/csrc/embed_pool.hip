@@ -340,6 +340,62 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
   }
 }
 
+// fp32 input, D % 4 == 0, windows of <= POOL_WIN patches (the CLIP features of the caption
+// steps): thread t owns columns 4t..4t+3 and issues its window's POOL_WIN 16-B loads at once
+// (pool_kernel moves 4 B per load instruction: 32 of them per thread at D = 768).  Same
+// per-column summation order as pool_kernel.
+__global__ __launch_bounds__(POOL_NT) void pool4_kernel(const float* __restrict__ in, void* out,
+                                                        int out_f32, int64_t L, int D, int side,
+                                                        int normalize) {
+  __shared__ float red[POOL_NT / 64];
+  const int64_t b = blockIdx.y;
+  const int o = blockIdx.x;
+  const float* base = in + b * L * (int64_t)D;
+  int r0 = 0, r1 = 1, c0 = 0, c1 = 1;
+  if (o > 0) {
+    const int i = (o - 1) >> 3, j = (o - 1) & 7;
+    r0 = (i * side) / 4;
+    r1 = ((i + 1) * side + 3) / 4;
+    c0 = (j * side) / 8;
+    c1 = ((j + 1) * side + 7) / 8;
+  }
+  const int wc = c1 - c0, nwin = (r1 - r0) * wc;
+  const float inv_cnt = 1.f / (float)nwin;
+  const int d = 4 * threadIdx.x;
+  const int dc = d < D ? d : 0;
+  float4 v[POOL_WIN];
+#pragma unroll
+  for (int t = 0; t < POOL_WIN; ++t) {
+    const int tc = t < nwin ? t : 0;
+    const int y = r0 + tc / wc, x = c0 + tc % wc;
+    const int64_t row = o == 0 ? 0 : 1 + (int64_t)y * side + x;
+    v[t] = *reinterpret_cast<const float4*>(base + row * D + dc);
+  }
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (o == 0) {
+    a[0] = v[0].x, a[1] = v[0].y, a[2] = v[0].z, a[3] = v[0].w;
+  } else {
+#pragma unroll
+    for (int t = 0; t < POOL_WIN; ++t)
+      if (t < nwin) a[0] += v[t].x, a[1] += v[t].y, a[2] += v[t].z, a[3] += v[t].w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] *= inv_cnt;
+  }
+  float ss = 0.f;
+  if (d < D) ss = a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
+  ss = block_sum<POOL_NT>(ss, red);
+  const float scale = normalize ? 1.f / fmaxf(sqrtf(ss), 1e-12f) : 1.f;
+  if (d >= D) return;
+  const int64_t orow = (b * 33 + o) * (int64_t)D;
+  if (out_f32) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + orow + d) =
+        make_float4(a[0] * scale, a[1] * scale, a[2] * scale, a[3] * scale);
+  } else {
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + orow + d) =
+        make_uint2(pack2(a[0] * scale, a[1] * scale), pack2(a[2] * scale, a[3] * scale));
+  }
+}
+
 // F.normalize(dim=-1, eps=1e-12) of bf16 / fp32 rows (D <= 1024), one block per row.
 template <typename T>
 __global__ __launch_bounds__(POOL_NT) void l2norm_rows_kernel(const T* __restrict__ in,
@@ -448,7 +504,20 @@ extern "C" int gvl_pool_clip_ex(const void* in, int32_t in_fp32, void* out, int3
   if (B == 0) return 0;
   dim3 grid(33, (unsigned)B);
   hipStream_t s = gvl::as_stream(stream);
-  if (in_fp32)
+  // pool4_kernel takes grids whose 32 windows all hold <= POOL_WIN patches (side 16: 4 x 2;
+  // side 14 has 4 x 3 windows and stays on pool_kernel)
+  int max_win = 0;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 8; ++j) {
+      const int nw = (((i + 1) * side + 3) / 4 - (i * side) / 4) * (((j + 1) * side + 7) / 8 - (j * side) / 8);
+      max_win = nw > max_win ? nw : max_win;
+    }
+  const bool win_ok = max_win <= POOL_WIN;
+  if (in_fp32 && D % 4 == 0 && gvl::aligned16(in) && win_ok &&
+      (out_fp32 ? gvl::aligned16(out) : reinterpret_cast<uintptr_t>(out) % 8 == 0))
+    hipLaunchKernelGGL(pool4_kernel, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in), out,
+                       (int)out_fp32, L, (int)D, side, (int)normalize);
+  else if (in_fp32)
     hipLaunchKernelGGL(pool_kernel<float>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
                        out, (int)out_fp32, L, (int)D, side, (int)normalize);
   else

@@ -304,35 +304,44 @@ __global__ __launch_bounds__(LN_BWD_NT) void ln_bwd_kernel(
   }
 }
 
-// Column reduction of the per-block partials: block = 16 columns x 64 partial groups; each
-// thread sums <= LN_BWD_MAXB/64 partials (all loads in flight), then the groups reduce in LDS.
-__global__ __launch_bounds__(1024) void ln_bwd_finalize(const float* __restrict__ ws, int nblk,
-                                                        int C, bf16_t* __restrict__ dw,
-                                                        bf16_t* __restrict__ db, int acc) {
-  __shared__ float red[64][17];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+// Column reduction of the per-block partials: block = 64 columns x 16 partial groups; each
+// thread sums <= LN_BWD_MAXB/16 partials (all loads in flight), a wave reading 256 contiguous
+// bytes of one partial row per load (16 columns x 64 groups read 64-B pieces of four rows:
+// 30 us for the LM's 25 deferred LayerNorms), then the groups reduce in LDS.  Both finalize
+// forms share it, so the deferred one stays bit-identical to the in-place one.
+constexpr int LN_FIN_COLS = 64, LN_FIN_GROUPS = 16;
+GVL_DEV void ln_fin_block(const float* __restrict__ ws, int nblk, int C, bf16_t* dw, bf16_t* db,
+                          int acc, float (&red)[LN_FIN_GROUPS][LN_FIN_COLS + 1]) {
+  const int cl = threadIdx.x & (LN_FIN_COLS - 1), g = threadIdx.x / LN_FIN_COLS;
+  const int c = blockIdx.x * LN_FIN_COLS + cl;
   float s = 0.f;
   if (c < 2 * C) {
-    float v[LN_BWD_MAXB / 64];
+    float v[LN_BWD_MAXB / LN_FIN_GROUPS];
 #pragma unroll
-    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) {
-      const int k = g + 64 * j;
+    for (int j = 0; j < LN_BWD_MAXB / LN_FIN_GROUPS; ++j) {
+      const int k = g + LN_FIN_GROUPS * j;
       v[j] = k < nblk ? ws[(int64_t)k * 2 * C + c] : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) s += v[j];
+    for (int j = 0; j < LN_BWD_MAXB / LN_FIN_GROUPS; ++j) s += v[j];
   }
   red[g][cl] = s;
   __syncthreads();
-  if (threadIdx.x >= 16 || c >= 2 * C) return;
+  if (threadIdx.x >= LN_FIN_COLS || c >= 2 * C) return;
   float t = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < 64; ++k) t += red[k][cl];
+#pragma unroll
+  for (int k = 0; k < LN_FIN_GROUPS; ++k) t += red[k][cl];
   bf16_t* dst = (c < C) ? (dw ? dw + c : nullptr) : (db ? db + (c - C) : nullptr);
   if (!dst) return;
   if (acc) t += bf2f(*dst);
   *dst = f2bf(t);
+}
+
+__global__ __launch_bounds__(1024) void ln_bwd_finalize(const float* __restrict__ ws, int nblk,
+                                                        int C, bf16_t* __restrict__ dw,
+                                                        bf16_t* __restrict__ db, int acc) {
+  __shared__ float red[LN_FIN_GROUPS][LN_FIN_COLS + 1];
+  ln_fin_block(ws, nblk, C, dw, db, acc, red);
 }
 
 // Batched form (gvl_layernorm_bwd_finalize_batched): blockIdx.y = item, each item as above.
@@ -344,33 +353,9 @@ struct LnFinBatch {
   int nblk[LN_FIN_MAX];
 };
 __global__ __launch_bounds__(1024) void ln_bwd_finalize_batched(LnFinBatch b, int C, int acc) {
-  __shared__ float red[64][17];
+  __shared__ float red[LN_FIN_GROUPS][LN_FIN_COLS + 1];
   const int it = blockIdx.y;
-  const float* __restrict__ ws = b.ws[it];
-  const int nblk = b.nblk[it];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  float s = 0.f;
-  if (c < 2 * C) {
-    float v[LN_BWD_MAXB / 64];
-#pragma unroll
-    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) {
-      const int k = g + 64 * j;
-      v[j] = k < nblk ? ws[(int64_t)k * 2 * C + c] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < LN_BWD_MAXB / 64; ++j) s += v[j];
-  }
-  red[g][cl] = s;
-  __syncthreads();
-  if (threadIdx.x >= 16 || c >= 2 * C) return;
-  float t = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < 64; ++k) t += red[k][cl];
-  bf16_t* dst = (c < C) ? (b.dw[it] ? b.dw[it] + c : nullptr) : (b.db[it] ? b.db[it] + (c - C) : nullptr);
-  if (!dst) return;
-  if (acc) t += bf2f(*dst);
-  *dst = f2bf(t);
+  ln_fin_block(b.ws[it], b.nblk[it], C, b.dw[it], b.db[it], acc, red);
 }
 
 // >= 2 rows per wave, <= LN_BWD_MAXB blocks (512: 2 per CU, 8 waves, ~16 rows in flight per CU).
@@ -457,7 +442,7 @@ static int ln_bwd_launch(const void* dy, int64_t lddy, const void* x, int64_t ld
                        mean, rstd, rp, ldr, dxp, lddx, (int)accumulate_dx, ws, rows, (int)cols);
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd");
   if (ws && !defer) {
-    const int g2 = (int)((2 * cols + 15) / 16);
+    const int g2 = (int)((2 * cols + LN_FIN_COLS - 1) / LN_FIN_COLS);
     hipLaunchKernelGGL(ln_bwd_finalize, dim3(g2), dim3(1024), 0, s, ws, nb, (int)cols,
                        static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), (int)accumulate_wb);
     GVL_LAUNCH_CHECK("gvl_layernorm_bwd(finalize)");
@@ -503,7 +488,7 @@ extern "C" int gvl_layernorm_bwd_finalize_batched(const float* const* ws, const 
     b.dw[i] = dw ? static_cast<bf16_t*>(dw[i]) : nullptr;
     b.db[i] = db ? static_cast<bf16_t*>(db[i]) : nullptr;
   }
-  const int g2 = (int)((2 * cols + 15) / 16);
+  const int g2 = (int)((2 * cols + LN_FIN_COLS - 1) / LN_FIN_COLS);
   hipLaunchKernelGGL(ln_bwd_finalize_batched, dim3(g2, count), dim3(1024), 0, gvl::as_stream(stream), b,
                      (int)cols, (int)(accumulate_wb & 1));
   GVL_LAUNCH_CHECK("gvl_layernorm_bwd_finalize_batched");

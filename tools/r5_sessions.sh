@@ -289,5 +289,22 @@ r5aq)  # attention prologues: fragment loads + first DMAs in one round trip, bra
     GVL_LIB=$LIB bench lm_${L}_$r lm; GVL_LIB=$LIB bench qf_${L}_$r qformer
   done; done
   ;;
+r5pl)  # 16-B CLIP pooling (pool4_kernel), coalesced LayerNorm finalize (64 columns x 16 groups) vs libgvl_old.so
+  ktests kt "layernorm or pool"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ln_one.py > $O/ln_${L}_$r.log 2>&1; fatal $? ln
+    echo "$L $r"; grep ln_bwd $O/ln_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/qf_table.txt; grep -E "pool|ln_" $O/qf_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
