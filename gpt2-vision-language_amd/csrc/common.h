@@ -56,10 +56,44 @@ GVL_DEV float warp_max(float v) {
   return v;
 }
 
+// Wave reductions without LDS round trips (__shfl_xor lowers to ds_bpermute_b32 plus an
+// lgkmcnt(0) wait per step): DPP within each 16-lane row (xor 1, xor 2, then the 8- and 16-lane
+// mirrors, each pairing two already-uniform halves), then the gfx950 row swaps (l ^ 16, l ^ 32),
+// all VALU.  Every step combines two equal-valued groups, so every lane ends with the same bits.
+template <int CTRL>
+GVL_DEV float dpp_src(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <bool MAX>
+GVL_DEV float dpp_op(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+template <bool MAX>
+GVL_DEV float row16_reduce(float v) {
+  v = dpp_op<MAX>(v, dpp_src<0xB1>(v));   // quad_perm [1,0,3,2]: l ^ 1
+  v = dpp_op<MAX>(v, dpp_src<0x4E>(v));   // quad_perm [2,3,0,1]: l ^ 2
+  v = dpp_op<MAX>(v, dpp_src<0x141>(v));  // row_half_mirror: the other quad of the 8
+  return dpp_op<MAX>(v, dpp_src<0x140>(v));  // row_mirror: the other 8 of the 16
+}
+template <bool MAX>
+GVL_DEV float swap16_reduce(float v) {  // op(v(l), v(l ^ 16))
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return dpp_op<MAX>(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+template <bool MAX>
+GVL_DEV float swap32_reduce(float v) {  // op(v(l), v(l ^ 32))
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return dpp_op<MAX>(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+GVL_DEV float wave_sum_v(float v) { return swap32_reduce<false>(swap16_reduce<false>(row16_reduce<false>(v))); }
+GVL_DEV float wave_max_v(float v) { return swap32_reduce<true>(swap16_reduce<true>(row16_reduce<true>(v))); }
+GVL_DEV float half_sum_v(float v) { return swap16_reduce<false>(row16_reduce<false>(v)); }  // per 32 lanes
+
 // Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
-template <int NT>
+// V: the wave step by wave_sum_v (VALU) instead of warp_sum (LDS permutes).
+template <int NT, bool V = false>
 GVL_DEV float block_sum(float v, float* red) {
-  v = warp_sum(v);
+  v = V ? wave_sum_v(v) : warp_sum(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __syncthreads();
   if (l == 0) red[w] = v;
@@ -69,9 +103,9 @@ GVL_DEV float block_sum(float v, float* red) {
   for (int i = 0; i < NT / 64; ++i) s += red[i];
   return s;
 }
-template <int NT>
+template <int NT, bool V = false>
 GVL_DEV float block_max(float v, float* red) {
-  v = warp_max(v);
+  v = V ? wave_max_v(v) : warp_max(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __syncthreads();
   if (l == 0) red[w] = v;

@@ -33,6 +33,10 @@ GVL_DEV void ce_store(bf16_t* p, uint4 v) {
   if constexpr (GVL_CE_STNT) __builtin_nontemporal_store(__builtin_bit_cast(ce_u32x4, v), reinterpret_cast<ce_u32x4*>(p));
   else *reinterpret_cast<uint4*>(p) = v;
 }
+// row max / sum wave steps by DPP + lane swaps (common.h wave_max_v / wave_sum_v); 0: LDS permutes
+#ifndef GVL_CE_DPP
+#define GVL_CE_DPP 1
+#endif
 constexpr int CE_MAXC = 8192 / CE_NT;  // 16-B chunks per thread: V <= 65536
 constexpr float CE_L2E = 1.4426950408889634f;
 
@@ -91,7 +95,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
       for (int k = 0; k < 4; ++k) mx = fmaxf(mx, fmaxf(lo_bf(w[k]), hi_bf(w[k])));
     }
   }
-  mx = block_max<CE_NT>(mx, red);
+  mx = block_max<CE_NT, GVL_CE_DPP>(mx, red);
   const float mxl = mx * CE_L2E;
   float s = 0.f;
 #pragma unroll
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(CE_NT) void ce_row_kernel(
              __builtin_amdgcn_exp2f(fmaf(hi_bf(w[k]), CE_L2E, -mxl));
     }
   }
-  s = block_sum<CE_NT>(s, red);
+  s = block_sum<CE_NT, GVL_CE_DPP>(s, red);
   const float lse = mx + __logf(s);
   if (tid == 0) row_loss[r] = lse - bf2f(src[tgt]);
   if (dst) {

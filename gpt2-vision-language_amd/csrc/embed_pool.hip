@@ -340,10 +340,11 @@ __global__ __launch_bounds__(POOL_NT) void pool_kernel(const TIn* __restrict__ i
   }
 }
 
-// fp32 input, D % 4 == 0, windows of <= POOL_WIN patches (the CLIP features of the caption
-// steps): thread t owns columns 4t..4t+3 and issues its window's POOL_WIN 16-B loads at once
-// (pool_kernel moves 4 B per load instruction: 32 of them per thread at D = 768).  Same
-// per-column summation order as pool_kernel.
+// fp32 input, D % 4 == 0, windows of <= WIN patches (the CLIP features of the caption steps:
+// side 16 -> 8, side 14 -> 12): thread t owns columns 4t..4t+3 and issues its window's WIN 16-B
+// loads at once (pool_kernel moves 4 B per load instruction: 32 of them per thread at D = 768).
+// Same per-column summation order as pool_kernel.
+template <int WIN>
 __global__ __launch_bounds__(POOL_NT) void pool4_kernel(const float* __restrict__ in, void* out,
                                                         int out_f32, int64_t L, int D, int side,
                                                         int normalize) {
@@ -363,9 +364,9 @@ __global__ __launch_bounds__(POOL_NT) void pool4_kernel(const float* __restrict_
   const float inv_cnt = 1.f / (float)nwin;
   const int d = 4 * threadIdx.x;
   const int dc = d < D ? d : 0;
-  float4 v[POOL_WIN];
+  float4 v[WIN];
 #pragma unroll
-  for (int t = 0; t < POOL_WIN; ++t) {
+  for (int t = 0; t < WIN; ++t) {
     const int tc = t < nwin ? t : 0;
     const int y = r0 + tc / wc, x = c0 + tc % wc;
     const int64_t row = o == 0 ? 0 : 1 + (int64_t)y * side + x;
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(POOL_NT) void pool4_kernel(const float* __restrict_
     a[0] = v[0].x, a[1] = v[0].y, a[2] = v[0].z, a[3] = v[0].w;
   } else {
 #pragma unroll
-    for (int t = 0; t < POOL_WIN; ++t)
+    for (int t = 0; t < WIN; ++t)
       if (t < nwin) a[0] += v[t].x, a[1] += v[t].y, a[2] += v[t].z, a[3] += v[t].w;
 #pragma unroll
     for (int e = 0; e < 4; ++e) a[e] *= inv_cnt;
@@ -504,19 +505,21 @@ extern "C" int gvl_pool_clip_ex(const void* in, int32_t in_fp32, void* out, int3
   if (B == 0) return 0;
   dim3 grid(33, (unsigned)B);
   hipStream_t s = gvl::as_stream(stream);
-  // pool4_kernel takes grids whose 32 windows all hold <= POOL_WIN patches (side 16: 4 x 2;
-  // side 14 has 4 x 3 windows and stays on pool_kernel)
+  // pool4_kernel<8 | 16> by the largest of the 32 windows (side 16: 4 x 2, side 14: 4 x 3)
   int max_win = 0;
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 8; ++j) {
       const int nw = (((i + 1) * side + 3) / 4 - (i * side) / 4) * (((j + 1) * side + 7) / 8 - (j * side) / 8);
       max_win = nw > max_win ? nw : max_win;
     }
-  const bool win_ok = max_win <= POOL_WIN;
-  if (in_fp32 && D % 4 == 0 && gvl::aligned16(in) && win_ok &&
-      (out_fp32 ? gvl::aligned16(out) : reinterpret_cast<uintptr_t>(out) % 8 == 0))
-    hipLaunchKernelGGL(pool4_kernel, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in), out,
-                       (int)out_fp32, L, (int)D, side, (int)normalize);
+  const bool vec_ok = in_fp32 && D % 4 == 0 && gvl::aligned16(in) &&
+                      (out_fp32 ? gvl::aligned16(out) : reinterpret_cast<uintptr_t>(out) % 8 == 0);
+  if (vec_ok && max_win <= 8)
+    hipLaunchKernelGGL(pool4_kernel<8>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
+                       out, (int)out_fp32, L, (int)D, side, (int)normalize);
+  else if (vec_ok && max_win <= 16)
+    hipLaunchKernelGGL(pool4_kernel<16>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
+                       out, (int)out_fp32, L, (int)D, side, (int)normalize);
   else if (in_fp32)
     hipLaunchKernelGGL(pool_kernel<float>, grid, dim3(POOL_NT), 0, s, static_cast<const float*>(in),
                        out, (int)out_fp32, L, (int)D, side, (int)normalize);

@@ -22,10 +22,20 @@ constexpr int LN_BWD_NT = 256;   // 4 waves, one row each (+1 prefetched)
 #endif
 constexpr int LN_BWD_MAXB = GVL_LN_BWD_MAXB;
 
-GVL_DEV float half_sum(float v) {
+// Row sums by DPP + lane swaps (common.h wave_sum_v / half_sum_v: no ds_bpermute round trips,
+// six per row sum in the __shfl_xor butterflies).
+#ifndef GVL_LN_DPP  // 0: the __shfl_xor butterflies (A/B builds)
+#define GVL_LN_DPP 1
+#endif
+GVL_DEV float half_sum(float v) {  // over the 32 lanes of this half-wave
+  if (GVL_LN_DPP) return half_sum_v(v);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+GVL_DEV float row_sum64(float v) {  // over the wave
+  if (GVL_LN_DPP) return wave_sum_v(v);
+  return warp_sum(v);
 }
 
 template <int IT>
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(LN_BWD_NT) void ln_bwd_kernel(
         for (int r = 0; r < 4; ++r) xh[it][r] = g[it][r] = 0.f;
       }
     }
-    const float m1 = warp_sum(s1) / (float)C, m2 = warp_sum(s2) / (float)C;
+    const float m1 = row_sum64(s1) / (float)C, m2 = row_sum64(s2) / (float)C;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int c = (lane + 64 * it) * 4;

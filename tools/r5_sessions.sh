@@ -306,5 +306,32 @@ r5pl)  # 16-B CLIP pooling (pool4_kernel), coalesced LayerNorm finalize (64 colu
     python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
   f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/qf_table.txt; grep -E "pool|ln_" $O/qf_table.txt
   ;;
+r5pl2)  # 16-B CLIP pooling for 12-patch windows too (side 14: the linear bridge's features)
+  ktests kt "pool"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "linear or qformer" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests edge "edge" tests/test_gpu_parity_full.py
+  for r in 1 2; do bench lin_$r linear; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lin -o lin -- \
+    python bench.py --workload linear --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lin.json 2> $O/prof_lin.err; fatal $? prof_lin
+  f=$(find $O/prof_lin -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lin_table.txt; grep -E "pool" $O/lin_table.txt
+  ;;
+r5dpp)  # LayerNorm / CE row reductions by DPP + lane swaps (no ds_bpermute) vs libgvl_nodpp.so; 16-B pooling at side 14
+  ktests kt "layernorm or pool or cross_entropy or lm_head"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2; do for L in base nodpp; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ln_one.py > $O/ln_${L}_$r.log 2>&1; fatal $? ln
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ce_one.py > $O/ce_${L}_$r.log 2>&1; fatal $? ce
+    echo "$L $r"; cat $O/ln_${L}_$r.log | grep -v amdgpu.ids; grep rows= $O/ce_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base nodpp; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lin_${L}_$r linear; GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lin -o lin -- \
+    python bench.py --workload linear --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lin.json 2> $O/prof_lin.err; fatal $? prof_lin
+  f=$(find $O/prof_lin -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lin_table.txt; grep -E "pool|ln_" $O/lin_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
