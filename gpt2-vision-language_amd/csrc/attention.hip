@@ -363,8 +363,7 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     float lt = l[g];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = swap32_reduce<false>(swap16_reduce<false>(lt));  // lanes l, l^16, l^32, l^48 (VALU swaps)
 #if GVL_ATTN_FWD_V2
     if constexpr (!DROP) lt = o[g][4][0];
 #endif
@@ -767,8 +766,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
 #pragma unroll
         for (int k = 0; k < 4; ++k) sd += lo_bf(ow[k]) * lo_bf(dw[k]) + hi_bf(ow[k]) * hi_bf(dw[k]);
       }
-      sd += __shfl_xor(sd, 16, 64);
-      sd += __shfl_xor(sd, 32, 64);
+      sd = swap32_reduce<false>(swap16_reduce<false>(sd));  // the row's 4 lanes (VALU swaps)
       Dq[g] = qok[g] ? sd : 0.f;
     }
   }
@@ -1122,8 +1120,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
   }
   if (!qok) Dq = 0.f;
   const float lse2 = qok ? lse_raw * LOG2E : 0.f;
-  Dq += __shfl_xor(Dq, 16, 64);
-  Dq += __shfl_xor(Dq, 32, 64);
+  Dq = swap32_reduce<false>(swap16_reduce<false>(Dq));  // the row's 4 lanes (VALU swaps)
   __syncthreads();
   float4_t sc[4], dp[4];
 #pragma unroll

@@ -333,5 +333,18 @@ r5dpp)  # LayerNorm / CE row reductions by DPP + lane swaps (no ds_bpermute) vs 
     python bench.py --workload linear --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lin.json 2> $O/prof_lin.err; fatal $? prof_lin
   f=$(find $O/prof_lin -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/lin_table.txt; grep -E "pool|ln_" $O/lin_table.txt
   ;;
+r5sw)  # attention D / row-sum lane reductions by VALU swaps (bit-identical) vs libgvl_old.so
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  for r in 1 2 3; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep -v amdgpu.ids $O/attn_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base old; do
+    LIB=$LIBDIR/libgvl.so; [ $L = old ] && LIB=$LIBDIR/libgvl_old.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
