@@ -1064,17 +1064,24 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
 // [query][key] tiles; phase 2 (wave w = keys 16w..16w+15) reads them transposed
 // (ds_read_b64_tr_b16 gives the same permuted k-slot order as the dK/dV kernel's registers) for
 // dV = P^T dO and dK = dS^T Q.  One launch instead of three, and S / dP computed once.
+// GVL_ATTN_SHORT_LDS32 (default 1): P and dS are written over the V and K tiles once every wave
+// is past its last K / V read (one more barrier), so a block needs 32 KiB of LDS instead of
+// 48: five blocks per CU instead of three (1536 (b, h) blocks: 1.2 rounds instead of 2).
+#ifndef GVL_ATTN_SHORT_LDS32
+#define GVL_ATTN_SHORT_LDS32 1
+#endif
 template <bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
-  // [Q, K, V, dO, P, dS] 64x64 bf16 tiles
-  __shared__ __attribute__((aligned(16))) char smem[6][KT * D * 2];
+  // [Q, K, V, dO(, P, dS)] 64x64 bf16 tiles
+  constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
+  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][KT * D * 2];
   char* const qs = smem[0];
   char* const ks = smem[1];
   char* const vs = smem[2];
   char* const ds = smem[3];
-  char* const ps = smem[4];
-  char* const ss = smem[5];
+  char* const ps = smem[0] + (L32 ? 2 : 4) * (KT * D * 2);  // (L32: over V)
+  char* const ss = smem[0] + (L32 ? 1 : 5) * (KT * D * 2);  // (L32: over K)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   const int64_t bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
@@ -1152,14 +1159,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
       sc[n][r] = pv * (dpv - Dq);  // dS
     }
   // P and dS to LDS as [query][key]: lane (query ql) owns keys 16n + 4Gl .. +3 (8 bytes)
+  uint2 pw[4], sw[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
-    const int off = swz_tr(ql, 2 * n + (Gl >> 1)) + (Gl & 1) * 8;
-    *reinterpret_cast<uint2*>(ps + off) =
-        make_uint2(pack2(pd[n][0], pd[n][1]), pack2(pd[n][2], pd[n][3]));
-    *reinterpret_cast<uint2*>(ss + off) =
-        make_uint2(pack2(sc[n][0], sc[n][1]), pack2(sc[n][2], sc[n][3]));
+    pw[n] = make_uint2(pack2(pd[n][0], pd[n][1]), pack2(pd[n][2], pd[n][3]));
+    sw[n] = make_uint2(pack2(sc[n][0], sc[n][1]), pack2(sc[n][2], sc[n][3]));
   }
+  auto store_p_ds = [&]() {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int off = swz_tr(ql, 2 * n + (Gl >> 1)) + (Gl & 1) * 8;
+      *reinterpret_cast<uint2*>(ps + off) = pw[n];
+      *reinterpret_cast<uint2*>(ss + off) = sw[n];
+    }
+  };
+  if constexpr (!L32) store_p_ds();
   {  // dQ = dS K (lane-local dS fragments, K read transposed)
     const short8_t sf0 = pack_frag(sc[0], sc[1]), sf1 = pack_frag(sc[2], sc[3]);
     float4_t acc[4];
@@ -1176,6 +1190,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
             make_uint2(pack2(acc[t][0] * p.scale, acc[t][1] * p.scale),
                        pack2(acc[t][2] * p.scale, acc[t][3] * p.scale));
     }
+  }
+  if constexpr (L32) {  // every wave past its K / V reads, then P / dS over them
+    __syncthreads();
+    store_p_ds();
   }
   __syncthreads();
   // phase 2: this lane's key; P^T / dS^T fragments in the dK/dV kernel's k-slot order

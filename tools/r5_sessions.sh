@@ -346,5 +346,19 @@ r5sw)  # attention D / row-sum lane reductions by VALU swaps (bit-identical) vs 
     GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross
   done; done
   ;;
+r5l32)  # short-sequence attention backward in 32 KiB of LDS (P / dS over V / K): 5 blocks per CU vs 3 (libgvl_l48.so)
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2 3; do for L in base l48; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep "B=128" $O/attn_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base l48; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lin_${L}_$r linear
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
