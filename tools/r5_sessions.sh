@@ -360,5 +360,18 @@ r5l32)  # short-sequence attention backward in 32 KiB of LDS (P / dS over V / K)
     GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lin_${L}_$r linear
   done; done
   ;;
+r5pf)  # LayerNorm backward two rows in flight ahead (GVL_LN_BWD_PF=2) vs one (libgvl_pf1.so)
+  ktests kt "layernorm"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for L in base pf1; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/ln_one.py > $O/ln_${L}_$r.log 2>&1; fatal $? ln
+    echo "$L $r"; grep ln_bwd $O/ln_${L}_$r.log
+  done; done
+  for r in 1 2; do for L in base pf1; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lm_${L}_$r lm
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
