@@ -85,7 +85,7 @@ r5f)  # Q-Former gradient probes vs the reference
   GVL_MARGINS_DIR=$O/parity_margins ktests probe "grad_probe" tests/test_gpu_parity_bench.py
   python -c "import json;print(json.dumps(json.load(open('$O/parity_margins/qformer_grad_probe.json')),indent=1))"
   ;;
-r5g|r5fin|r5fin2|r5fin3|r5fin4|r5fin5)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
+r5g|r5fin|r5fin2|r5fin3|r5fin4|r5fin5|r5fin6)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
   suite
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
   python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],[(k,d[k]['value']) for k in d if k.startswith('caption')])"
