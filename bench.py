@@ -15,6 +15,7 @@ resident in HBM before timing; weights random-init with the reference's init rec
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -504,6 +505,10 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        # graphs holding RCCL work are released (and the device drained) before the
+        # communicator goes
+        gc.collect()
+        torch.cuda.synchronize()
         dist.barrier()
         dist.destroy_process_group()
 

@@ -7,6 +7,7 @@
   * two ranks on the one GPU over gloo with gvl modules + gvl AdamW (CFG3 / CFG5 at
     world size 2): the DP step equals one process over the concatenated batch.
 """
+import gc
 import os
 import socket
 
@@ -151,6 +152,7 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         mbs, loss_fn, build = _cap_batches(cuda, 2, seed=21), CAP_LOSS, lambda: _qformer(cuda, nl)
         cuts = lambda m: list(m.bridge.layers)[1:]  # noqa: E731
     _world1(cuda)
+    gs = None
     try:
         ref = build()
         ropt = ref.configure_optimizers(0.1, 1e-3, "cuda")
@@ -183,6 +185,11 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         rb.remove()
         b.remove()
     finally:
+        # the captured segments hold RCCL work: release them (and let the device drain) before
+        # the communicator goes — one run aborted in destroy_process_group with them still alive
+        gs = None
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()
 
 
