@@ -373,5 +373,19 @@ r5pf)  # LayerNorm backward two rows in flight ahead (GVL_LN_BWD_PF=2) vs one (l
     GVL_LIB=$LIB bench qf_${L}_$r qformer; GVL_LIB=$LIB bench cross_${L}_$r cross; GVL_LIB=$LIB bench lm_${L}_$r lm
   done; done
   ;;
+r5one)  # single-tile short forward (16 KiB, 6 waves/SIMD; libgvl_w5.so: 5) vs the two-stage kernel (GVL_ATTN_FWD_ONE=0)
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2 3; do for v in base w5 off; do
+    LIB=$LIBDIR/libgvl.so; [ $v = w5 ] && LIB=$LIBDIR/libgvl_w5.so; ONE=1; [ $v = off ] && ONE=0
+    GVL_LIB=$LIB GVL_ATTN_FWD_ONE=$ONE timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${v}_$r.log 2>&1; fatal $? attn
+    echo "attn $v $r"; grep -E "Tq=63|Tq=31" $O/attn_${v}_$r.log
+  done; done
+  for r in 1 2; do for v in base off; do
+    ONE=1; [ $v = off ] && ONE=0
+    GVL_ATTN_FWD_ONE=$ONE bench qf_${v}_$r qformer; GVL_ATTN_FWD_ONE=$ONE bench cross_${v}_$r cross; GVL_ATTN_FWD_ONE=$ONE bench lin_${v}_$r linear
+  done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
