@@ -15,7 +15,6 @@ resident in HBM before timing; weights random-init with the reference's init rec
 from __future__ import annotations
 
 import argparse
-import gc
 import json
 import os
 import sys
@@ -352,7 +351,8 @@ def cpu_baseline(workload, seconds=15.0, max_steps=6):
     """The oracle (fp32 CPU restatement of the reference step, pinned to the reference's
     fixtures) on this host's cores: zero_grad -> fwd -> bwd -> clip -> AdamW, repeated for
     ~`seconds` of CPU work.  Sample: LM = BASELINE configs[0] itself (B=4 x T=1024);
-    captions = B=32 images of the B=128 step (z (32,257,768) pooled, 31 text tokens)."""
+    captions = the bench's own B=128 step (z (128,257,768) pooled, 31 text
+    tokens), timed from its first step (one B=128 oracle step is ~4-5 s of CPU work)."""
     from oracle import models as OM
     from oracle import ops as O
     O.FAST_PATHS = True  # the torch ops the reference itself calls (oracle/ops.py)
@@ -379,7 +379,7 @@ def cpu_baseline(workload, seconds=15.0, max_steps=6):
     else:
         from gvl.train import caption_batch, caption_labels
         from oracle import ops as O
-        B = 32
+        B = 128
         z, xx, yy, mm = caption_batch(B, device="cpu")
         zp = O.pool_clip(z)
         lab = caption_labels(yy, mm)
@@ -393,7 +393,8 @@ def cpu_baseline(workload, seconds=15.0, max_steps=6):
             P["gpt.transformer.wte.weight"] = P["gpt.lm_head.weight"]
             loss_of = lambda P_, it: OM.caption_forward(P_, kind, zp, xx, 12, 12, 1024, lab)[1]
         sample = f"{workload} caption step, B={B} images (fp32 oracle restatement)"
-    OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)  # warm-up
+    if workload == "lm":
+        OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
         OM.train_steps(P, kind, train, loss_of, 1, lambda it: 1e-4)
@@ -505,12 +506,12 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        # graphs holding RCCL work are released (and the device drained) before the
-        # communicator goes
-        gc.collect()
-        torch.cuda.synchronize()
+        # the library's teardown: every captured step is closed (bucket work joined, device
+        # drained, graphs reset) before the communicator goes
+        from gvl.dist import close_graphed_steps, destroy_process_group
+        close_graphed_steps()
         dist.barrier()
-        dist.destroy_process_group()
+        destroy_process_group()
 
 
 if __name__ == "__main__":

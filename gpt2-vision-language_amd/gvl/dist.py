@@ -311,6 +311,29 @@ def segment_cuts(model, blocks_per_segment: int = None):
     return []
 
 
+def close_graphed_steps(group=None):
+    """Close every live gvl.graph.GraphedStep (all of them, or those bound to `group`)."""
+    from .graph import live_steps
+    for st in live_steps():
+        if group is None or st.pg is group or st.pg is None:
+            st.close()
+
+
+def destroy_process_group(group=None):
+    """The reference scripts' teardown (train_gpt2.py:523, gpt2_linear/train.py:372,
+    gpt2_cross-att/train.py:348) with gvl's captured steps released first.
+
+    Order: close every live GraphedStep (joins its last replay's bucket work, drains the
+    device, resets its graphs and memory pool), drain the device, then destroy the
+    communicator.  Nothing of a captured step outlives the process group it was replayed
+    against, whatever the caller's garbage-collection order."""
+    close_graphed_steps(group)
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.destroy_process_group(group)
+
+
 def all_reduce_mean_(t, group=None):
     """The per-step scalar loss all-reduce (C3)."""
     if dist.is_initialized() and dist.get_world_size(group) > 1:

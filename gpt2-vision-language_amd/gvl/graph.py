@@ -26,8 +26,18 @@ segment captured as its own graph in one shared memory pool:
 Replay: A_0, then for each segment the all-reduces of the buckets the previous segment
 finalised (recorded at capture time) are issued on RCCL's stream before A_j is replayed,
 so they run while A_j's kernels do; the rest, the scalar loss all-reduce and B follow.
+
+Teardown (the reference ends every train script with destroy_process_group():
+train_gpt2.py:523, gpt2_linear/train.py:372, gpt2_cross-att/train.py:348): `close()`
+joins the step's outstanding bucket work, drains the device, resets every captured graph
+(frees the private memory pool) and drops the references to the optimizer, buckets and
+process group; a weakref finalizer does the same when a step is collected unclosed.
+`gvl.dist.destroy_process_group()` closes every live GraphedStep before it destroys the
+communicator, so a drop-in script's teardown never depends on garbage-collection order.
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 
@@ -36,6 +46,26 @@ import torch.distributed as dist
 from . import kernels as K
 from .dist import all_reduce_mean_
 from .train import StepResult, finish, train_step
+
+
+_LIVE = weakref.WeakSet()  # GraphedSteps not yet closed (gvl.dist.destroy_process_group)
+
+
+def _release(graphs, dev):
+    """Finalizer / close(): drain the device, then reset the captured graphs (their
+    executable graphs and the private memory pool go with the last reset)."""
+    try:
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize(dev)
+    finally:
+        for g in graphs:
+            g.reset()
+        graphs.clear()
+
+
+def live_steps():
+    """GraphedSteps created and not closed yet (tests / teardown)."""
+    return list(_LIVE)
 
 
 class GraphedStep:
@@ -48,10 +78,15 @@ class GraphedStep:
         than lr (betas, eps, weight_decay, max_norm) are frozen into the graph."""
         self.model, self.opt = model, optimizer
         self.pg = process_group
+        self.buckets = None
+        self._all_graphs = []  # every captured graph, in capture order (close() resets them)
         world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         # segmented=True forces the two-graph DP form (tests drive it at world size 1)
         self.dp = buckets is not None and (world > 1 if segmented is None else segmented)
         dev = next(model.parameters()).device
+        self.device = dev
+        self._finalizer = weakref.finalize(self, _release, self._all_graphs, dev)
+        _LIVE.add(self)
         self.seed_off = K.seed_offset(dev)
         K._gemm_workspace(dev)
         K._gemm_tickets(dev)
@@ -66,6 +101,7 @@ class GraphedStep:
         torch.cuda.synchronize(dev)
         if not self.dp:
             self.graph = torch.cuda.CUDAGraph()
+            self._all_graphs.append(self.graph)
             with torch.cuda.graph(self.graph):
                 res = train_step(model, optimizer, micro_batches, loss_fn, None, max_norm=max_norm)
                 self.seed_off.add_(1)
@@ -86,6 +122,7 @@ class GraphedStep:
             pool = self.graphs[0].pool() if self.graphs else None
             g.capture_begin(*(() if pool is None else (pool,)))
             self.graphs.append(g)
+            self._all_graphs.append(g)
             self.logs.append([])
             buckets.capture_log = self.logs[-1]
 
@@ -112,6 +149,7 @@ class GraphedStep:
                 self.graphs[-1].capture_end()
                 buckets.capture_log = None
                 self.graph_b = torch.cuda.CUDAGraph()
+                self._all_graphs.append(self.graph_b)
                 self.graph_b.capture_begin(self.graphs[0].pool())
                 norm = finish(optimizer, None, max_norm)
                 self.seed_off.add_(1)
@@ -123,9 +161,42 @@ class GraphedStep:
         self.buckets = buckets
         self.result = StepResult(loss_accum, norm)
 
+    @property
+    def closed(self) -> bool:
+        return not self._finalizer.alive
+
+    def close(self):
+        """Release the captured step before its process group goes (idempotent).
+
+        Order: join the bucket all-reduces the last replay issued (the current stream waits
+        for RCCL's stream), drain the device, reset every graph (executable graphs and the
+        shared private pool), then drop the references to the buckets and process group.
+        After close() the step cannot be replayed."""
+        if self.closed:
+            return
+        _LIVE.discard(self)
+        try:
+            if self.buckets is not None:
+                self.buckets.join()
+        finally:
+            self._finalizer()  # _release: synchronize + reset every graph
+            self.graphs = self.logs = []
+            self.graph = self.graph_b = None
+            self.buckets = self.pg = None
+            self.result = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def __call__(self, lr) -> StepResult:
         """One optimizer step at learning rate `lr` (every param group, like
         train_gpt2.py:474-475).  Returns device scalars (no host sync)."""
+        if self.closed:
+            raise RuntimeError("GraphedStep.__call__ after close()")
         for g in self.opt.param_groups:
             g["lr"] = lr
         self.opt.advance()

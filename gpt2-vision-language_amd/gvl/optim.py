@@ -26,6 +26,36 @@ def _pad(n):
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def arena_offsets(param_groups):
+    """(offsets in param_groups order, per-group [start, end) segments, total) of the flat
+    arenas: each parameter a 16-B aligned slot, group after group (decay group first)."""
+    offs, seg = [], []
+    total = 0
+    for g in param_groups:
+        start = total
+        # parameters tagged with the same `_gvl_stack_key` (the cross-att blocks' kv_proj
+        # weights / biases, which gvl.functional.CrossKVFn multiplies as ONE stacked matrix)
+        # get consecutive arena slots at the first one's place, so the stack is a view of the
+        # arena instead of a per-step torch.cat; the param_groups order (and so the optimizer
+        # state_dict's parameter indices) is unchanged
+        stacks = {}
+        for p in g["params"]:
+            k = getattr(p, "_gvl_stack_key", None)
+            if k is not None:
+                stacks.setdefault(k, []).append(p)
+        placed = {}
+        for p in g["params"]:
+            if id(p) in placed:
+                continue
+            k = getattr(p, "_gvl_stack_key", None)
+            for q in (stacks[k] if k is not None else [p]):
+                placed[id(q)] = total
+                total += _pad(q.numel())
+        offs.extend(placed[id(p)] for p in g["params"])
+        seg.append((start, total))
+    return offs, seg, total
+
+
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW drop-in (the reference's fused AdamW, train_gpt2.py:140-143).
 
@@ -57,30 +87,7 @@ class AdamW(torch.optim.Optimizer):
             if p.dtype != BF16:
                 raise TypeError("gvl AdamW expects bf16 parameters (the reference trains the "
                                 "model after .to(torch.bfloat16))")
-        offs, seg = [], []
-        total = 0
-        for g in self.param_groups:
-            start = total
-            # parameters tagged with the same `_gvl_stack_key` (the cross-att blocks' kv_proj
-            # weights / biases, which gvl.functional.CrossKVFn multiplies as ONE stacked matrix)
-            # get consecutive arena slots at the first one's place, so the stack is a view of the
-            # arena instead of a per-step torch.cat; the param_groups order (and so the optimizer
-            # state_dict's parameter indices) is unchanged
-            stacks = {}
-            for p in g["params"]:
-                k = getattr(p, "_gvl_stack_key", None)
-                if k is not None:
-                    stacks.setdefault(k, []).append(p)
-            placed = {}
-            for p in g["params"]:
-                if id(p) in placed:
-                    continue
-                k = getattr(p, "_gvl_stack_key", None)
-                for q in (stacks[k] if k is not None else [p]):
-                    placed[id(q)] = total
-                    total += _pad(q.numel())
-            offs.extend(placed[id(p)] for p in g["params"])
-            seg.append((start, total))
+        offs, seg, total = arena_offsets(self.param_groups)
         total = max(total, _ALIGN)
         sdt = F32 if self.master_weights else BF16
         parena = torch.zeros(total, dtype=BF16, device=dev)
@@ -130,11 +137,16 @@ class AdamW(torch.optim.Optimizer):
         return self._arena["g"]
 
     def arena_layout(self):
-        """[(param, offset, numel)] in arena order (used by gvl.dist buckets)."""
+        """[(param, offset, numel)] sorted by arena offset (used by gvl.dist buckets).
+
+        Offsets follow param_groups order except for parameters sharing a
+        `_gvl_stack_key`, which take consecutive slots at the first one's position; sorting
+        keeps the "arena order" contract GradBuckets relies on when it has no model."""
         if self._arena is None:
             self._build()
         a = self._arena
-        return [(p, o, p.numel()) for p, o in zip(a["params"], a["offs"])]
+        return sorted(((p, o, p.numel()) for p, o in zip(a["params"], a["offs"])),
+                      key=lambda e: e[1])
 
     def master_of(self, p):
         """fp32 master copy of parameter p (None with master_weights=False)."""

@@ -389,3 +389,90 @@ def test_backward_segments_shared_input_backpropagated_once(n_layers):
     for (name, p), pr in zip(m.named_parameters(), ref.parameters()):
         assert torch.allclose(p.grad, pr.grad, atol=1e-6), name
         assert fired.count(name) == 1, (name, fired)
+
+
+def test_destroy_process_group_closes_live_steps():
+    """gvl.dist.destroy_process_group (the reference scripts' teardown, train_gpt2.py:523)
+    closes every live captured step bound to the group before the communicator goes, in that
+    order, whatever the caller's garbage-collection order (host logic; GraphedStep itself
+    needs a GPU: tests/test_gpu_dp.py::test_segmented_graph_step_matches_eager)."""
+    import gvl.dist as D
+    import gvl.graph as G
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    order = []
+
+    class FakeStep:  # the part of GraphedStep the teardown relies on
+        pg = None
+
+        def close(self):
+            order.append(("close", dist.is_initialized()))
+            G._LIVE.discard(self)
+
+    st = FakeStep()
+    G._LIVE.add(st)
+    try:
+        assert st in G.live_steps()
+        D.destroy_process_group()
+    finally:
+        G._LIVE.discard(st)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    assert order == [("close", True)]  # closed while the group was still alive
+    assert not dist.is_initialized() and st not in G.live_steps()
+
+
+@pytest.mark.parametrize("stacked", [False, True])
+def test_stacked_arena_layout_buckets(stacked):
+    """gvl.optim.arena_offsets with `_gvl_stack_key` (the cross-att kv_proj stack): stacked
+    parameters take consecutive slots, slots tile the arena without overlap, and GradBuckets
+    built from the offset-sorted layout (no model: the arena order is the ready-order proxy)
+    covers every parameter once, with runs that are exactly the union of their slots
+    (arena_layout's order contract with stacked placement)."""
+    from gvl.dist import GradBuckets
+    from gvl.optim import _pad, arena_offsets
+    torch.manual_seed(0)
+    lins = [torch.nn.Linear(24, 16) for _ in range(5)]
+    if stacked:
+        for li in lins[1:4]:
+            li.weight._gvl_stack_key = "kv_w"
+            li.bias._gvl_stack_key = "kv_b"
+    groups = [{"params": [li.weight for li in lins]}, {"params": [li.bias for li in lins]}]
+    offs, seg, total = arena_offsets(groups)
+    params = [p for g in groups for p in g["params"]]
+    off_of = {id(p): o for p, o in zip(params, offs)}
+    slots = sorted((o, o + _pad(p.numel())) for p, o in zip(params, offs))
+    assert slots[0][0] == 0 and slots[-1][1] == total
+    assert all(a[1] == b[0] for a, b in zip(slots, slots[1:]))  # tiled, no overlap
+    if stacked:
+        ow = [off_of[id(li.weight)] for li in lins[1:4]]
+        assert all(b - a == _pad(lins[1].weight.numel()) for a, b in zip(ow, ow[1:]))
+
+    class Opt:
+        def __init__(self):
+            self._g = torch.zeros(total)
+            self._layout = sorted(((p, o, p.numel()) for p, o in zip(params, offs)),
+                                  key=lambda e: e[1])
+
+        def arena_layout(self):
+            return self._layout
+
+        @property
+        def grad_arena(self):
+            return self._g
+
+    bk = GradBuckets(Opt(), bucket_mb=3 * 24 * 16 * 4 / 2**20)
+    try:
+        seen = [p for _, ps in bk.buckets for p in ps]
+        assert len(seen) == len(params) and {id(p) for p in seen} == {id(p) for p in params}
+        for runs, ps in bk.buckets:
+            covered = sorted((off_of[id(p)], off_of[id(p)] + _pad(p.numel())) for p in ps)
+            merged = []
+            for a, b in covered:
+                if merged and merged[-1][1] == a:
+                    merged[-1][1] = b
+                else:
+                    merged.append([a, b])
+            assert [tuple(r) for r in merged] == list(runs)
+    finally:
+        bk.remove()

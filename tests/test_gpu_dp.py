@@ -7,7 +7,6 @@
   * two ranks on the one GPU over gloo with gvl modules + gvl AdamW (CFG3 / CFG5 at
     world size 2): the DP step equals one process over the concatenated batch.
 """
-import gc
 import os
 import socket
 
@@ -142,7 +141,8 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
     qformer3: a 3-layer bridge, two cuts that both read the projected image tokens — vis_proj's
     gradient must be back-propagated once, in the last segment (BackwardSegments.backward)."""
     from gvl.dist import GradBuckets
-    from gvl.graph import GraphedStep
+    from gvl.dist import destroy_process_group as gvl_destroy
+    from gvl.graph import GraphedStep, live_steps
     from gvl.train import train_step
     if kind == "lm":
         mbs, loss_fn, build = _lm_batches(cuda, 3, seed=11), LM_LOSS, lambda: _gpt(cuda)
@@ -151,8 +151,15 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         nl = 3 if kind == "qformer3" else 2
         mbs, loss_fn, build = _cap_batches(cuda, 2, seed=21), CAP_LOSS, lambda: _qformer(cuda, nl)
         cuts = lambda m: list(m.bridge.layers)[1:]  # noqa: E731
+    import gvl.dist as D
     _world1(cuda)
     gs = None
+    real_avg, captured = D._avg, []
+
+    def spy_avg(t, pg, async_op):  # every collective the step issues, and whether a capture was live
+        captured.append(torch.cuda.is_current_stream_capturing())
+        return real_avg(t, pg, async_op)
+    D._avg = spy_avg
     try:
         ref = build()
         ropt = ref.configure_optimizers(0.1, 1e-3, "cuda")
@@ -168,7 +175,12 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
         logged = [len(x) for x in gs.logs]
         print("buckets per segment", logged, "of", len(b.buckets))
         assert logged[0] >= 1 and sum(logged) == len(b.buckets)
+        n_before = len(captured)
         loss = gs(1e-3).loss.item()
+        # no collective is ever issued inside a capture; the replay issues each
+        # bucket's all-reduce eagerly between the segment graphs
+        assert captured and not any(captured), captured
+        assert len(captured) - n_before >= len(b.buckets)
         torch.cuda.synchronize()
         print("eager", losses_ref, "graphed step 3", loss)
         assert loss == pytest.approx(losses_ref[2], rel=1e-6)
@@ -184,13 +196,15 @@ def test_segmented_graph_step_matches_eager(cuda, kind):
             assert e < 1e-3, (n, e)
         rb.remove()
         b.remove()
+        # the library's teardown: close() releases the graphs; gvl.dist.destroy_process_group
+        # closes any step still live (none here) before destroying the communicator
+        gs.close()
+        assert gs.closed and gs not in live_steps()
+        with pytest.raises(RuntimeError):
+            gs(1e-3)
     finally:
-        # the captured segments hold RCCL work: release them (and let the device drain) before
-        # the communicator goes — one run aborted in destroy_process_group with them still alive
-        gs = None
-        gc.collect()
-        torch.cuda.synchronize()
-        dist.destroy_process_group()
+        D._avg = real_avg
+        gvl_destroy()
 
 
 def _rank_main(rank, world, port, kind, graphed, q):

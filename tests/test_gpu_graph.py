@@ -62,6 +62,16 @@ def test_graphed_lm_step_matches_eager(cuda):
     for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
         assert torch.equal(p1, p2), n
     assert o2._step_count == 3
+    # lifecycle: close() resets the graph (idempotent), a closed step refuses to replay,
+    # and the weights it trained stay usable eagerly
+    from gvl.graph import live_steps
+    assert gs in live_steps()
+    gs.close()
+    gs.close()
+    assert gs.closed and gs not in live_steps()
+    with pytest.raises(RuntimeError):
+        gs(lrs[0])
+    assert torch.isfinite(train_step(m2, o2, b2, loss_fn, lrs[0]).loss).item()
 
 
 def test_graphed_dropout_masks_advance(cuda):
