@@ -275,7 +275,7 @@ def pmc_record(workload, kernel):
     clock; {} when not measured."""
     try:
         with open(TRAFFIC_FILE) as f:
-            t = json.load(f)["workloads"][{"lm": "lm", "qformer": "qf"}[workload]]
+            t = json.load(f)["workloads"][{"qformer": "qf"}.get(workload, workload)]
         return t[kernel]
     except (OSError, KeyError, ValueError):
         return {}

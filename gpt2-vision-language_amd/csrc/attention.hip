@@ -1070,52 +1070,71 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
 #ifndef GVL_ATTN_SHORT_LDS32
 #define GVL_ATTN_SHORT_LDS32 1
 #endif
+struct ShortIn {  // one (b, h)'s operands of the short backward, loaded ahead of its math
+  uint4 rq[2], rk[2], rv[2], rd[2], oa[2];
+  float lse_raw;
+};
 template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
-  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
-  // [Q, K, V, dO(, P, dS)] 64x64 bf16 tiles
-  constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
-  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][KT * D * 2];
-  char* const qs = smem[0];
-  char* const ks = smem[1];
-  char* const vs = smem[2];
-  char* const ds = smem[3];
-  char* const ps = smem[0] + (L32 ? 2 : 4) * (KT * D * 2);  // (L32: over V)
-  char* const ss = smem[0] + (L32 ? 1 : 5) * (KT * D * 2);  // (L32: over K)
+GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn& in) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
-  const int64_t bh = blockIdx.x, b = bh / p.H, h = bh - b * p.H;
+  const int64_t b = bh / p.H, h = bh - b * p.H;
   const bf16_t* qbase = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* kbase = p.k + b * p.k_sb + h * p.k_sh;
   const bf16_t* vbase = p.v + b * p.v_sb + h * p.v_sh;
   const bf16_t* obase = p.o + b * p.o_sb + h * p.o_sh;
   const bf16_t* dobase = gg.dout + b * gg.do_sb + h * gg.do_sh;
-  // every global operand of the block issued before the first wait (branch-free loads)
+  // every global operand of the (b, h) issued before the first wait (branch-free loads)
+  const int ql = wave * 16 + (lane & 15);
+  const bool qok = ql < p.Tq;
+  const int qlc = qok ? ql : 0;
+  load_rows_nb(in.rq, qbase, p.q_st, p.Tq, tid);
+  load_rows_nb(in.rk, kbase, p.k_st, p.Tk, tid);
+  load_rows_nb(in.rv, vbase, p.v_st, p.Tk, tid);
+  load_rows_nb(in.rd, dobase, gg.do_st, p.Tq, tid);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) in.oa[c] = reinterpret_cast<const uint4*>(obase + qlc * p.o_st + 16 * Gl)[c];
+  in.lse_raw = p.lse[bh * p.Tq + qlc];
+}
+
+// One (b, h) of the short backward from its loaded operands (bwd_short_load); smem: 4 (L32) or
+// 6 tiles of 64 x 64 bf16.
+template <bool DROP>
+GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const ShortIn& in,
+                            char* smem0, uint64_t seed_) {
+  constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
+  constexpr int TB = KT * D * 2;
+  char* const qs = smem0;
+  char* const ks = smem0 + TB;
+  char* const vs = smem0 + 2 * TB;
+  char* const ds = smem0 + 3 * TB;
+  char* const ps = smem0 + (L32 ? 2 : 4) * TB;  // (L32: over V)
+  char* const ss = smem0 + (L32 ? 1 : 5) * TB;  // (L32: over K)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Gl = lane >> 4;
+  const int64_t b = bh / p.H, h = bh - b * p.H;
   const int ql = wave * 16 + (lane & 15);
   const bool qok = ql < p.Tq;
   const int64_t ridx = bh * p.Tq + ql;
-  const int qlc = qok ? ql : 0;
-  uint4 rq[2], rk[2], rv[2], rd[2], oa[2], da[2];
-  load_rows_nb(rq, qbase, p.q_st, p.Tq, tid);
-  load_rows_nb(rk, kbase, p.k_st, p.Tk, tid);
-  load_rows_nb(rv, vbase, p.v_st, p.Tk, tid);
-  load_rows_nb(rd, dobase, gg.do_st, p.Tq, tid);
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    oa[c] = reinterpret_cast<const uint4*>(obase + qlc * p.o_st + 16 * Gl)[c];
-    da[c] = reinterpret_cast<const uint4*>(dobase + qlc * gg.do_st + 16 * Gl)[c];
-  }
-  const float lse_raw = p.lse[bh * p.Tq + qlc];
-  short8_t qf[2], df[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    qf[s2] = load_frag_global_nb(qbase, p.q_st, ql, s2, lane, qok);
-    df[s2] = load_frag_global_nb(dobase, gg.do_st, ql, s2, lane, qok);
-  }
+  const uint4 (&rq)[2] = in.rq, (&rk)[2] = in.rk, (&rv)[2] = in.rv, (&rd)[2] = in.rd;
+  const uint4 (&oa)[2] = in.oa;
+  const float lse_raw = in.lse_raw;
   store_rows<false>(rq, qs, tid);
   store_rows<false>(rk, ks, tid);
   store_rows<false>(rv, vs, tid);
   store_rows<false>(rd, ds, tid);
+  __syncthreads();
+  // this lane's Q / dO fragments and dO row piece from the LDS tiles (rows past Tq hold row 0,
+  // as load_rows_nb staged them: the data the global fragment loads used to fetch)
+  short8_t qf[2], df[2];
+  uint4 da[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    qf[s2] = frag_row(qs, 16 * wave, s2, lane);
+    df[s2] = frag_row(ds, 16 * wave, s2, lane);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) da[c] = *reinterpret_cast<const uint4*>(ds + swz_row(ql, 2 * Gl + c));
   // phase 1: this lane's query, its D (4 lanes x 16 dims of dO . O) and log-sum-exp
   float Dq = 0.f;
 #pragma unroll
@@ -1128,7 +1147,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
   if (!qok) Dq = 0.f;
   const float lse2 = qok ? lse_raw * LOG2E : 0.f;
   Dq = swap32_reduce<false>(swap16_reduce<false>(Dq));  // the row's 4 lanes (VALU swaps)
-  __syncthreads();
   float4_t sc[4], dp[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -1227,6 +1245,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg
           make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
     }
   }
+}
+
+// (Round 6 measured two (b, h) per block, the second one's loads issued before the first one's
+// math, at 3 waves per SIMD: no faster — T = 63 0.023-0.024 vs 0.023 ms, T = 32 with dropout
+// 0.020 vs 0.018 ms; Q-Former / cross / linear steps 0.1-0.9 % slower; profiles/r6/
+// attn_short_pair_r6d.txt — and was removed.)
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
+  const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
+  constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
+  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][KT * D * 2];
+  ShortIn in;
+  bwd_short_load<DROP>(p, gg, blockIdx.x, in);
+  bwd_short_item<DROP>(p, gg, blockIdx.x, in, smem[0], seed_);
 }
 
 int fill(const gvl_attn_desc* d, AttnP& p) {

@@ -46,6 +46,77 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
     *reinterpret_cast<uint4*>(lds + (t * NWV + wave) * 1024 + lane * 16) = v[t];
 }
 
+// 96-wide B slab of a 32-deep K-step (gemm_w4n_kernel: 128 x 96 tiles).
+// 6 KiB of operand in 1-KiB pieces over 4 waves: pieces j = 4t + wave, j < 6 real; waves 2-3's
+// second piece (j = 6, 7) is a dummy whose buffer offset is out of range (the load returns
+// zeros without touching memory) and whose LDS write lands in a 2 KiB pad no fragment reads,
+// so every wave runs the same branch-free staging code.
+//  * K-contiguous (the weight in forward GEMMs): [96 rows][32] 64-B rows, the Step image;
+//  * MN-contiguous (the weight in dX): cols 0-63 as [32][64] 128-B rows (Step192's tail image,
+//    f2 swizzle), cols 64-95 as [32][32] 64-B rows at +4 KiB, chunk c of k-row kr at
+//    c ^ f3(kr): the ds_read_b64_tr_b16 lane groups of the fragment pattern below hit 32
+//    distinct 8-B bank pairs (checked exhaustively, like attn_swizzle_check.py).
+constexpr uint32_t W4_OOB = 0x7FFFFFF0u;
+GVL_DEV int f3(int k) { return (k >> 2) & 2; }  // 64-B rows
+template <bool MN, int NWV = 4>
+struct Step96 {
+  static constexpr int R = 96;
+  static constexpr int REAL = 6;
+  static constexpr int BYTES = 8 * 1024;  // 6 KiB image + 2 KiB pad for the dummy pieces
+  static constexpr int PER = 2;
+  static_assert(NWV == 4, "four waves");
+  GVL_DEV static int64_t elem(int64_t ld, int64_t r0, int64_t k0, int j, int lane) {
+    if (!MN) {
+      const int row = 16 * j + (lane >> 2);
+      return (r0 + row) * ld + k0 + ((lane & 3) ^ f64b(row)) * 8;
+    }
+    if (j < 4) {
+      const int kr = 8 * j + (lane >> 3);
+      return (k0 + kr) * ld + r0 + ((lane & 7) ^ f2(kr)) * 8;
+    }
+    const int kr = 16 * (j - 4) + (lane >> 2);
+    return (k0 + kr) * ld + r0 + 64 + ((lane & 3) ^ f3(kr)) * 8;
+  }
+  GVL_DEV static void base_offsets(int64_t ld, int64_t r0, int64_t k0, int wave, int lane,
+                                   int (&off)[PER]) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int j = t * NWV + wave;
+      off[t] = j < REAL ? (int)(elem(ld, r0, k0, j, lane) * 2) : (int)W4_OOB;
+    }
+  }
+  GVL_DEV static int step_bytes(int64_t ld) { return MN ? (int)(KS * ld * 2) : KS * 2; }
+  GVL_DEV static short8_t frag(const char* lds, int c0, int lane) {
+    if (!MN) {
+      const int row = c0 + (lane & 15), ch = lane >> 4;
+      return *reinterpret_cast<const short8_t*>(lds + row * 64 + ((ch ^ f64b(row)) << 4));
+    }
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int kr = 8 * G + q;
+    short8_t r;
+    if (c0 < 64) {
+      const int ch = (c0 >> 3) + (p >> 1);
+      const int off1 = kr * 128 + ((ch ^ f2(kr)) << 4) + (p & 1) * 8;
+      r.lo = lds_read_tr(lds + off1);
+      r.hi = lds_read_tr(lds + off1 + 4 * 128);
+    } else {
+      const int ch = ((c0 - 64) >> 3) + (p >> 1);
+      const int off1 = kr * 64 + ((ch ^ f3(kr)) << 4) + (p & 1) * 8;
+      r.lo = lds_read_tr(lds + 4096 + off1);
+      r.hi = lds_read_tr(lds + 4096 + off1 + 4 * 64);
+    }
+    return r;
+  }
+};
+template <int BN, bool MN>
+struct W4SlabB {
+  using type = Step<BN, MN, 4>;
+};
+template <bool MN>
+struct W4SlabB<96, MN> {
+  using type = Step96<MN>;
+};
+
 // K-steps are 32 deep; the register staging runs P = 3 steps ahead of the LDS writes, the LDS
 // ring holds NS = 3 steps (the one being read, the next, the one being written).  Step c:
 //   read the fragments of step c+1 (written and published by the previous barrier);
@@ -95,9 +166,10 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                            \
   } while (0)
 #elif GVL_W4_IGLP == 3  // PA+PB rounds of {MFMA, read, MFMA, read, MFMA, load, MFMA, write}
+// (at most FM * FN / 4 rounds: the 128 x 96 tile has 12 MFMAs per step for 4 loads)
 #define W4_INTERLEAVE()                                                           \
   do {                                                                            \
-    _Pragma("unroll") for (int q_ = 0; q_ < PA + PB; ++q_) {                      \
+    _Pragma("unroll") for (int q_ = 0; q_ < (PA + PB < FM * FN / 4 ? PA + PB : FM * FN / 4); ++q_) { \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                          \
@@ -136,13 +208,14 @@ GVL_DEV void w4_store(char* lds, const uint4* v, int wave, int lane) {
 
 // BM = 192 (6 x 4 fragments per wave) or 128 (4 x 4): the 128-row tile fills the chip when
 // 192-row tiles would leave over a quarter of the CUs idle (3968 / 4096-row caption GEMMs).
-template <int NS, bool BMN, int EPI, int BM>
+template <int NS, bool BMN, int EPI, int BM, int BN = W4_BN>
 __device__ __forceinline__ void gemm_w4_body(const GemmP& p) {
-  constexpr int BN = W4_BN, NW = 4, FM = BM / 32, FN = 4, P = 3;
+  constexpr int NW = 4, FM = BM / 32, FN = BN / 32, P = 3;
   static_assert(NS == 3, "ring geometry");
   static_assert(BM == 192 || BM == 128, "tile rows");
+  static_assert(BN == 128 || (BN == 96 && BM == 128), "tile columns");
   using SA = Step<BM, false, NW>;
-  using SB = Step<BN, BMN, NW>;
+  using SB = typename W4SlabB<BN, BMN>::type;
   constexpr int SLOT = SA::BYTES + SB::BYTES;
   constexpr int PA = SA::PER, PB = SB::PER;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -374,6 +447,10 @@ template <int NS, bool BMN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4m_kernel(GemmP p) {
   gemm_w4_body<NS, BMN, EPI, 128>(p);
 }
+template <int NS, bool BMN, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4n_kernel(GemmP p) {
+  gemm_w4_body<NS, BMN, EPI, 128, 96>(p);
+}
 
 #ifndef GVL_W4_NS
 #define GVL_W4_NS 3
@@ -390,17 +467,19 @@ int w4_group(int dflt) {
   return g > 0 ? g : dflt;
 }
 
-template <bool BMN, int EPI, int BM>
+template <bool BMN, int EPI, int BM, int BN = W4_BN>
 int launch_w4_bm(const GemmP& p0, hipStream_t s) {
   constexpr int NS = GVL_W4_NS;
   GemmP p = p0;
   p.tiles_m = (int)((p.M + BM - 1) / BM);
-  p.tiles_n = (int)((p.N + W4_BN - 1) / W4_BN);
+  p.tiles_n = (int)((p.N + BN - 1) / BN);
   p.splits = 1;
   p.kper = p.K;
   p.group = w4_group(p.group);
-  constexpr int lds = NS * (BM + W4_BN) * KS * 2;
-  auto kern = BM == 192 ? gemm_w4_kernel<GVL_W4_NS, BMN, EPI> : gemm_w4m_kernel<GVL_W4_NS, BMN, EPI>;
+  constexpr int slot = BM * KS * 2 + W4SlabB<BN, BMN>::type::BYTES;
+  constexpr int lds = NS * slot;
+  auto kern = BN == 96 ? gemm_w4n_kernel<GVL_W4_NS, BMN, EPI>
+              : BM == 192 ? gemm_w4_kernel<GVL_W4_NS, BMN, EPI> : gemm_w4m_kernel<GVL_W4_NS, BMN, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -424,8 +503,30 @@ bool w4_use128(const GemmP& p) {
   return on && t192 * 4 < cus * 3 && t128 > t192 && t128 <= cus;
 }
 
+// 128 x 96 tiles (gemm_w4n_kernel) where 128-row tiles are used and 96-column ones fill more
+// of the chip in one round: the cross-att decoder's 3968 text rows (186 -> 248 tiles at
+// N = 768) and the Q-Former bridge's 4096 query rows (192 -> 256).  A CU streams 224 operand
+// rows per K-step instead of 256 for its (smaller) tile, so a one-round launch of these shapes,
+// paced by the per-CU operand stream, ends ~1/8 sooner.  Measured
+// (profiles/r6/w4n_bn96_r6c.txt, 3968 / 4096 rows): the forward products (K-contiguous weight)
+// gain 8-10 % (attn.c_proj + bias + residual 16.3 -> 14.5 us, mlp.c_proj 39.1 -> 35.3), the dX
+// ones (MN-contiguous weight, whose 32-column image is fetched as 64-B row segments) lose 6-8 %
+// (c_fc.dX 35.8 -> 38.5), so only K-contiguous B takes them (GVL_W4_BN96=2: both, A/B).
+// GVL_W4_BN96=0: 128 x 128 as before (A/B).
+bool w4_use96(const GemmP& p, bool b_mn) {
+  static const int mode = [] {
+    const char* e = getenv("GVL_W4_BN96");
+    return e ? atoi(e) : 1;
+  }();
+  if (mode == 0 || (b_mn && mode < 2) || !w4_use128(p)) return false;
+  const int64_t cus = gvl::num_cus(), tm = (p.M + 127) / 128;
+  const int64_t t128 = tm * ((p.N + 127) / 128), t96 = tm * ((p.N + 95) / 96);
+  return t96 > t128 && t96 <= cus;
+}
+
 template <bool BMN, int EPI>
 int launch_w4(const GemmP& p, hipStream_t s) {
+  if (w4_use96(p, BMN)) return launch_w4_bm<BMN, EPI, 128, 96>(p, s);
   return w4_use128(p) ? launch_w4_bm<BMN, EPI, 128>(p, s) : launch_w4_bm<BMN, EPI, 192>(p, s);
 }
 
@@ -503,6 +604,7 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
 }
 
 bool gemm_w4_rows128(const GemmP& p) { return w4_use128(p); }
+bool gemm_w4_cols96(const GemmP& p, bool b_mn) { return w4_use96(p, b_mn); }
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
   if (gemm_w4d_ok(p)) {

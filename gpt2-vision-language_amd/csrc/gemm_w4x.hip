@@ -420,8 +420,35 @@ __global__ __launch_bounds__(256, 1) void gemm_w4x_kernel(GemmP p) {
   gemm_w4x_body<BM, BN, AMN, BMN, EPI, GR>(p);
 }
 
+// Weight-gradient launches (AMN && BMN: the LM's batched / grouped dW over 16384 tokens, 3-7
+// rounds of whole-K tiles) and their grid (the grouped launch reads 2.16x its
+// operand bytes).  The three 256-column tiles that share a dY slab sit next to each other in an
+// XCD's work range, but in a persistent grid (one workgroup per CU walking vid += G) each starts
+// when ITS CU finished its previous tile, so after a few rounds the siblings are far apart and
+// the slab is fetched again by the late one.  GVL_W4X_NP=1: one workgroup per tile instead
+// (grid = tiles); the XCD's dispatcher hands the next tile of its contiguous range to the first
+// CU that frees up, so siblings start within one tile-retire of each other in every round.
+// GVL_W4X_DW_GROUP=n: tile rows per L2 group of the dW tile walk (default: the GEMM's).
+int w4x_np_mode() {
+  static const int v = [] {
+    const char* e = getenv("GVL_W4X_NP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+int w4x_dw_group(int dflt) {
+  static const int v = [] {
+    const char* e = getenv("GVL_W4X_DW_GROUP");
+    return e ? atoi(e) : 0;
+  }();
+  return v > 0 ? v : dflt;
+}
+
 template <int BM, int BN, bool AMN, bool BMN, int EPI, bool GR = false>
-void launch_w4x(const GemmP& p, hipStream_t s) {
+void launch_w4x(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  constexpr bool DW = AMN && BMN;
+  if constexpr (DW) p.group = w4x_dw_group(p.group);
   auto kern = gemm_w4x_kernel<BM, BN, AMN, BMN, EPI, GR>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -429,7 +456,8 @@ void launch_w4x(const GemmP& p, hipStream_t s) {
     attr_set = true;
   }
   const int total = GR ? p.gtile[p.batch] : p.tiles_m * p.tiles_n * p.batch;
-  const int grid = total < gvl::num_cus() ? total : gvl::num_cus();
+  const bool np = DW ? w4x_np_mode() >= 1 : w4x_np_mode() >= 2;
+  const int grid = (np || total < gvl::num_cus()) ? total : gvl::num_cus();
   constexpr int lds = x_ns<BM>() * (BM + BN) * KS * 2;
   gvl::launch_timed(kern, dim3(grid), dim3(256), lds, s, p);
 }

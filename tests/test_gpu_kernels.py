@@ -534,13 +534,30 @@ def test_gemm_tile128x192(cuda, a_mn, b_mn, epi, M, N, K):
 W4D_EPIS = ("plain", "bias", "bias_res", "res_inplace", "drop_res")
 
 
-def _w4_name(M, K, epi):
+def _w4_tiles(M, N, b_mn=0, cus=256):
+    """(128-row tiles?, 128 x 96 tiles?) as gemm_w4.hip's w4_use128 / w4_use96 decide (96-column
+    tiles for a K-contiguous B only, unless GVL_W4_BN96=2)."""
+    tn = -(-N // 128)
+    t192, t128 = -(-M // 192) * tn, -(-M // 128) * tn
+    r128 = t192 * 4 < cus * 3 and t128 > t192 and t128 <= cus
+    t96 = -(-M // 128) * -(-N // 96)
+    mode = int(os.environ.get("GVL_W4_BN96", "1"))
+    c96 = r128 and mode != 0 and (not b_mn or mode >= 2) and t128 < t96 <= cus
+    return r128, c96
+
+
+def _w4_name(M, K, epi, N=768, b_mn=0):
     """Kernel the default four-wave routing picks (GVL_W4D unset): the direct-A variant
-    (gemm_w4d.h) when K is a multiple of six 64-deep steps and the epilogue is one of its."""
+    (gemm_w4d.h) when K is a multiple of six 64-deep steps and the epilogue is one of its;
+    128-row tiles where 192-row ones fill under 3/4 of the chip, 128 x 96 ones (gemm_w4n_kernel)
+    where those fill more of it in one round."""
     mode = os.environ.get("GVL_W4D", "1")
-    rows = "m" if M <= 4096 else ""
+    r128, c96 = _w4_tiles(M, N, b_mn)
+    rows = "m" if r128 else ""
     direct = K % 384 == 0 and epi in W4D_EPIS and mode != "0" and (mode == "2" or not rows)
-    return f"gemm_w4d{rows}_kernel" if direct else f"gemm_w4{rows}_kernel"
+    if direct:
+        return f"gemm_w4d{rows}_kernel"
+    return "gemm_w4n_kernel" if c96 else f"gemm_w4{rows}_kernel"
 
 
 @pytest.mark.parametrize("b_mn", [0, 1])
@@ -595,7 +612,7 @@ def test_gemm_w4(cuda, b_mn, epi, M, N, K):
         _lib.lib().gvl_gemm_tune(3, -1)
     # 128-row tiles (gemm_w4m_kernel / gemm_w4dm_kernel) where 192-row ones would fill < 3/4
     # of the CUs; the direct-A variant where K % 384 == 0 and its epilogue is instantiated
-    assert name.startswith(_w4_name(M, K, epi)), name
+    assert name.startswith(_w4_name(M, K, epi, N, b_mn)), name
     assert rel_err(y.float().cpu().numpy(), ref.detach().numpy()) < 8e-3
     if epi == "bias_act_d":
         assert rel_err(kw["pre_out"].float().cpu().numpy(), x.grad.numpy()) < 8e-3
@@ -772,7 +789,7 @@ def test_gemm_dropout_gate(cuda):
     assert 0.08 < frac < 0.12
 
 
-@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, _w4_name(4096, 768, "drop_res")),
+@pytest.mark.parametrize("M,N,Kd,kern", [(4096, 768, 768, _w4_name(4096, 768, "drop_res", 768)),
                                          (4096, 3072, 768, "gemm_pp3_kernel"),
                                          (200, 136, 72, None), (4096, 768, 3072, None)])
 def test_gemm_bias_dropout_residual(cuda, M, N, Kd, kern):
@@ -1050,7 +1067,8 @@ def _attn_case(cuda, B, H, Tq, Tk, causal, packed, drop_p=0.0, seed=0, grad=True
         assert e < 2.5e-2, f"{nm} rel err {e}"
 
 
-@pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (2, 2, 300), (3, 12, 63), (2, 3, 64), (1, 1, 7)])
+@pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (2, 2, 300), (3, 12, 63), (2, 3, 64), (1, 1, 7),
+                                   (3, 3, 50), (40, 12, 31)])
 def test_attention_causal(cuda, B, H, T):
     _attn_case(cuda, B, H, T, T, True, packed=True)
 
@@ -1063,6 +1081,17 @@ def test_attention_noncausal(cuda, Tq, Tk):
 @pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130)])
 def test_attention_dropout_exact_mask(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False, drop_p=0.1, seed=4242)
+
+
+def test_attention_short_over_nan_filled_memory(cuda):
+    """The single-launch short backward (Q / dO fragments and the dO row piece of D read back
+    from its LDS tiles) repeated over NaN-filled free memory, causal 63-token and dropout 32 x 33
+    cases: any byte read before it is written shows up as an intermittent error."""
+    for it in range(6):
+        junk = torch.full((32 << 20,), float("nan"), device=cuda)
+        del junk
+        _attn_case(cuda, 4, 6, 63, 63, True, packed=True)
+        _attn_case(cuda, 3, 2, 32, 33, False, packed=False, drop_p=0.1, seed=77 + it)
 
 
 def test_attention_bwd_repeats_over_nan_filled_memory(cuda):

@@ -71,7 +71,9 @@ def main(root):
                      "clock / 2.4 GHz = MFMA-pipe cycles per dispatch-duration cycle at the 2.4 GHz peak "
                      "clock (exact either way)",
            "workloads": {}}
-    for wl in ("lm", "qf"):
+    wls = sorted({os.path.basename(d).rsplit("_FETCH_SIZE", 1)[0]
+                  for d in glob.glob(os.path.join(root, "*_FETCH_SIZE"))})
+    for wl in wls:
         fe = load(os.path.join(root, f"{wl}_FETCH_SIZE"), "FETCH_SIZE")
         wr = load(os.path.join(root, f"{wl}_WRITE_SIZE"), "WRITE_SIZE")
         mc = mfma_clock(root, wl)

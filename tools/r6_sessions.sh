@@ -1,0 +1,83 @@
+#!/bin/bash
+# Round-6 GPU sessions (run on the GPU box through gpurun): bash tools/r6_sessions.sh <name>.
+# Every GPU step has its own time limit; a session stops at the first failing step.
+# Each session names the bound it tests (only levers with a committed
+# predicted gain >= 3 % of a step get GPU minutes).
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; S=${1:?session}; O=gpurun_out/$S; mkdir -p $O
+LIBDIR=gpt2-vision-language_amd/gvl
+fatal() { [ "$1" -eq 0 ] || { echo "fatal rc $1 at $2"; exit $1; }; }
+suite() {  # GPU suite (margins recorded) + smoke
+  GVL_MARGINS_DIR=$O/parity_margins timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf \
+    --timeout 300 --timeout-method thread -p no:cacheprovider > $O/suite.log 2>&1
+  rc=$?; echo "suite rc=$rc"; tail -3 $O/suite.log; fatal $rc suite
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc $(tail -1 $O/smoke.log)"; fatal $rc smoke
+}
+ktests() {  # ktests <log> <pytest -k expression> [file]
+  timeout -k 10 600 python -u -m pytest ${3:-tests/test_gpu_kernels.py} -q -x -k "$2" --timeout 300 \
+    --timeout-method thread -p no:cacheprovider > $O/$1.log 2>&1; rc=$?; echo "$1: $(tail -1 $O/$1.log)"; fatal $rc $1
+}
+bench() {  # bench <tag> <workload> [steps]   (env passes through)
+  local a="--workload $2 --steps ${3:-10} --warmup 3"; [ $2 = lm ] && a="--steps ${3:-2} --warmup 1 --no-secondary"
+  timeout -k 10 300 python bench.py $a --no-cpu-baseline > $O/$1.json 2> $O/$1.err; fatal $? bench_$1
+  echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
+}
+case $S in
+r6a)  # teardown (GraphedStep.close, gvl.dist.destroy_process_group) tests; two-stream overlap probe
+      # (bound for the Q-Former two-branch lever: up to the 20 % non-GEMM share if half-batch chains
+      # overlap); DEFER_LMHEAD peak memory
+  ktests dp "" tests/test_gpu_dp.py
+  ktests graph "" tests/test_gpu_graph.py
+  for v in 1 0; do
+    GVL_W4_BM128=$v timeout -k 10 200 python -u tools/concurrency_probe.py 20 > $O/probe_bm128_$v.log 2>&1; fatal $? probe
+    echo "== probe GVL_W4_BM128=$v"; grep -v amdgpu.ids $O/probe_bm128_$v.log
+  done
+  for v in 1 0; do GVL_DEFER_LMHEAD=$v bench lm_d$v lm; done
+  ;;
+r6b)  # LM grouped dW launch: one workgroup per tile (GVL_W4X_NP=1) so the three tiles sharing a
+      # dY slab start together every round. Bound: the launch is 20.7 % of the LM step at 1.81 GHz
+      # and 2.16x its operand bytes; back at the dX kernels' 2.45 GHz it would be ~26 % shorter
+      # (5 % of the step); predicted gain >= 3 % only if traffic drops toward 1.4x and the clock
+      # follows. Kernel tests + bench-shape LM parity with NP=1, LM A/B alternated, PMC of the launch.
+  GVL_W4X_NP=1 ktests kt "grouped or w4x or wgrad or batched"
+  GVL_W4X_NP=1 GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for v in 0 1; do GVL_W4X_NP=$v bench lm_np${v}_$r lm; done; done
+  GVL_W4X_NP=1 GVL_W4X_DW_GROUP=1 bench lm_np1g1 lm
+  for v in 0 1; do for c in FETCH_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+    d=${c%% *}
+    GVL_W4X_NP=$v timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $O/pmc_np$v/lm_$d -o run -- \
+      python bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --no-graph > $O/pmc_np${v}_$d.log 2>&1; fatal $? pmc
+  done; done
+  ;;
+r6c)  # 128 x 96 four-wave tiles (gemm_w4n_kernel) for the 3968 / 4096-row N = 768 GEMMs. Bound: the
+      # cross step's w4m classes are 29.4 % at 186 tiles (one round, paced by the per-CU operand
+      # stream); 248 tiles streaming 224 instead of 256 rows each -> ~12 % off those kernels =
+      # ~3.7 % of the cross step, ~0.7 % of the Q-Former step (bridge rows)
+  ktests kt "test_gemm_w4 or gated or dropout_residual or grouped"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "cross or qformer" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "cross or qformer" tests/test_gpu_parity_full.py
+  for M in 3968 4096; do for v in 1 0; do
+    GVL_W4_BN96=$v GVL_DIAG_COLS=epi timeout -k 10 240 python -u tools/gemm_diag.py $M narrow > $O/diag_bn96_${v}_$M.log 2>&1; fatal $? diag
+    echo "== M=$M BN96=$v"; grep "N=" $O/diag_bn96_${v}_$M.log
+  done; done
+  for r in 1 2; do for v in 1 0; do GVL_W4_BN96=$v bench cross_b${v}_$r cross; GVL_W4_BN96=$v bench qf_b${v}_$r qformer; done; done
+  ;;
+r6d)  # short attention backward: two (b, h) per block with the second's loads issued before the
+      # first's math (GVL_ATTN_SHORT_PAIR=1) vs one per block. Bound: attn_bwd_short is 5.1 % of the
+      # Q-Former step, 4.9 % of linear, 6.4 % of cross at ~3.5 TB/s of its 99 MB; at 5.5 TB/s -> ~35 %
+      # off it = 1.7-2.2 % of those steps. Also: 128 x 96 tiles on K-contiguous B only (default now).
+  ktests kt "attention or attn or test_gemm_w4 or gated or dropout_residual"
+  GVL_W4_BN96=2 ktests kt96 "test_gemm_w4 and not w4x"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in 1 0; do
+    GVL_ATTN_SHORT_PAIR=$v timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_p${v}_$r.log 2>&1; fatal $? attn
+    echo "attn pair=$v $r"; grep -E "Tq=63|Tq=31|Tq=32" $O/attn_p${v}_$r.log
+  done; done
+  for r in 1 2; do for v in 1 0; do
+    GVL_ATTN_SHORT_PAIR=$v bench qf_p${v}_$r qformer; GVL_ATTN_SHORT_PAIR=$v bench cross_p${v}_$r cross; GVL_ATTN_SHORT_PAIR=$v bench lin_p${v}_$r linear
+  done; done
+  ;;
+*) echo "unknown session $S"; exit 2 ;;
+esac
