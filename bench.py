@@ -285,7 +285,7 @@ def pmc_traffic(workload, kernel):
     return pmc_record(workload, kernel).get("hbm_bytes")
 
 
-def dominant_kernel(summary, workload="lm", steps=1):
+def dominant_kernel(summary, workload="lm", steps=1, full=False):
     """Roofline of the GEMM instance with the largest total time.  Durations come from HIP
     events bound to each kernel's own dispatch (gvl.kernels.KernelTimer, dispatch=True):
     the interval rocprofv3's kernel trace reports for the same kernel name.  Also lists the
@@ -318,7 +318,13 @@ def dominant_kernel(summary, workload="lm", steps=1):
                                     / (sum(v["ms"] for v in summary.values()) * 1e-3) / 1e12
                                     / PEAK_BF16_TFLOPS, 4),
                 gemm_ms_per_step=round(sum(v["ms"] for v in summary.values()) / steps, 3),
-                top_gemms=table)
+                top_gemms=table,
+                # --gemm-table: every GEMM instance of the step (tools/qformer_budget.py)
+                **({"all_gemms": [dict(kernel=k, launches_per_step=round(v["launches"] / steps, 2),
+                                       avg_us=round(v["ms"] / v["launches"] * 1e3, 2),
+                                       gflop_per_launch=round(v["flops"] / v["launches"] / 1e9, 3))
+                                  for k, v in sorted(summary.items(), key=lambda kv: -kv[1]["ms"])]}
+                   if full else {}))
 
 
 # ---------------------------------------------------------------------- CPU baseline
@@ -439,6 +445,8 @@ def main():
                     help="CPU work per cpu_baseline sample (LM; captions get half)")
     ap.add_argument("--no-kernel-pass", action="store_true",
                     help="skip the eager per-GEMM timing pass (profiling runs)")
+    ap.add_argument("--gemm-table", action="store_true",
+                    help="list every GEMM instance of the step in roofline.all_gemms")
     ap.add_argument("--no-graph", action="store_true",
                     help="eager steps (default: the step is captured into hipGraphs; at N>1 two "
                          "graphs around the RCCL gradient all-reduce)")
@@ -459,7 +467,7 @@ def main():
     timer = None if args.no_kernel_pass else K.KernelTimer()
     dt, res = timed(step, args.steps, args.warmup, world, timer, graph=use_graph)
     value = units * args.steps / dt
-    roof = dominant_kernel(timer.summary(), args.workload, steps=1) if timer else None
+    roof = dominant_kernel(timer.summary(), args.workload, steps=1, full=args.gemm_table) if timer else None
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -492,7 +500,8 @@ def main():
                                      / world, 4),
                 loss=round(cres[0], 5), config=ccfg,
                 peak_hbm_gib=round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
-                roofline=dominant_kernel(ctimer.summary(), kind, steps=3) if ctimer else None)
+                roofline=dominant_kernel(ctimer.summary(), kind, steps=3, full=args.gemm_table)
+                if ctimer else None)
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 line["cpu_baseline"] = cpu_baseline(kind, seconds=args.cpu_seconds / 2)
             out[f"caption_{kind}"] = line

@@ -79,5 +79,13 @@ r6d)  # short attention backward: two (b, h) per block with the second's loads i
     GVL_ATTN_SHORT_PAIR=$v bench qf_p${v}_$r qformer; GVL_ATTN_SHORT_PAIR=$v bench cross_p${v}_$r cross; GVL_ATTN_SHORT_PAIR=$v bench lin_p${v}_$r linear
   done; done
   ;;
+r6e)  # Q-Former floor budget inputs: every GEMM instance of the step with its
+      # FLOP (bench --gemm-table) and the rocprofv3 kernel table at this head; same for the LM
+  timeout -k 10 300 python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline --gemm-table > $O/qf_gemms.json 2> $O/qf_gemms.err; fatal $? qf_gemms
+  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-secondary --no-cpu-baseline --gemm-table > $O/lm_gemms.json 2> $O/lm_gemms.err; fatal $? lm_gemms
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 45 > $O/qf_table.txt; head -30 $O/qf_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
