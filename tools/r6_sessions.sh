@@ -87,5 +87,23 @@ r6e)  # Q-Former floor budget inputs: every GEMM instance of
     python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
   f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 45 > $O/qf_table.txt; head -30 $O/qf_table.txt
   ;;
+r6fin|r6fin2|r6fin3)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
+  suite
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],[(k,d[k]['value']) for k in d if k.startswith('caption')])"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_qf -o qf -- \
+    python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lm -o lm -- \
+    python bench.py --steps 1 --warmup 1 --no-secondary --no-cpu-baseline > $O/prof_lm.json 2> $O/prof_lm.err; fatal $? prof_lm
+  for w in cross linear; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o $w -- \
+      python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_$w.json 2> $O/prof_$w.err; fatal $? prof_$w
+  done
+  for w in qf lm cross linear; do f=$(find $O/prof_$w -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 40 > $O/${w}_table.txt; head -8 $O/${w}_table.txt; done
+  ;;
+r6pmc|r6pmc2)  # PMC passes (FETCH / WRITE / MFMA busy + clock) of all four bench workloads at the head
+  timeout -k 10 1100 bash tools/pmc_traffic.sh $S "lm qf cross linear"; fatal $? pmc
+  python -c "import json;d=json.load(open('gpurun_out/pmc_traffic_$S.json'));[print(w, k, v['hbm_bytes'], v.get('mfma_busy'), v.get('clock_ghz')) for w in d['workloads'] for k, v in list(d['workloads'][w].items())[:2]]"
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
