@@ -1070,6 +1070,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
 #ifndef GVL_ATTN_SHORT_LDS32
 #define GVL_ATTN_SHORT_LDS32 1
 #endif
+// GVL_ATTN_SHORT_DIAG=1: timing-only build of the short backward (wrong results; never the shipped
+// library): every load, then dQ / dK / dV stores of the loaded bytes — the kernel's memory floor.
+#ifndef GVL_ATTN_SHORT_DIAG
+#define GVL_ATTN_SHORT_DIAG 0
+#endif
 struct ShortIn {  // one (b, h)'s operands of the short backward, loaded ahead of its math
   uint4 rq[2], rk[2], rv[2], rd[2], oa[2];
   float lse_raw;
@@ -1119,6 +1124,19 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
   const uint4 (&rq)[2] = in.rq, (&rk)[2] = in.rk, (&rv)[2] = in.rv, (&rd)[2] = in.rd;
   const uint4 (&oa)[2] = in.oa;
   const float lse_raw = in.lse_raw;
+  if constexpr (GVL_ATTN_SHORT_DIAG == 1) {  // timing-only: the loads, then stores of the same bytes
+    uint32_t x = in.oa[0].x ^ in.oa[1].y ^ __float_as_uint(lse_raw);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+      if (row < p.Tq) {
+        *reinterpret_cast<uint4*>(gg.dq + b * gg.dq_sb + h * gg.dq_sh + row * gg.dq_st + ch * 8) = rq[it] ^ make_uint4(x, x, x, x);
+        *reinterpret_cast<uint4*>(gg.dk + b * gg.dk_sb + h * gg.dk_sh + row * gg.dk_st + ch * 8) = rk[it] ^ rd[it];
+        *reinterpret_cast<uint4*>(gg.dv + b * gg.dv_sb + h * gg.dv_sh + row * gg.dv_st + ch * 8) = rv[it];
+      }
+    }
+    return;
+  }
   store_rows<false>(rq, qs, tid);
   store_rows<false>(rk, ks, tid);
   store_rows<false>(rv, vs, tid);

@@ -134,6 +134,11 @@ GVL_DEV float gelu_tanh_sig(float x, float x2) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * fmaf(B, x2, A)));
 }
 GVL_DEV float gelu_tanh(float x) { return x * gelu_tanh_sig(x, x * x); }
+// CLIP's quick-GELU x * sigmoid(1.702 x) (transformers QuickGELUActivation), one exp + rcp
+GVL_DEV float quick_gelu(float x) {
+  constexpr float A = 1.702f * 1.4426950408889634f;
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-A * x));
+}
 GVL_DEV float dgelu_tanh(float x) {
   // d/dx x s(2u) = s + 2 k0 x s (1 - s) (1 + 3 k1 x^2)
   constexpr float C = 2.f * 0.7978845608028654f, D = 3.f * 0.044715f * C;

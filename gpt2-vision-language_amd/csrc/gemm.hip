@@ -255,7 +255,7 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
     const int cfg = env().cfg;
     if ((cfg < 0 || cfg == 10) && gvl::gemm_w4_plan(p, d->a_mn, cfg == 10)) {
       // (cfg 11: default routing with the four-wave kernel off)
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14"};
       if (gvl::gemm_w4d_ok(p))
         snprintf(buf, len, "%s<%s, %s>", gvl::gemm_w4_rows128(p) ? "gemm_w4dm_kernel" : "gemm_w4d_kernel",
                  tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
@@ -265,7 +265,7 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
                  : gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
                  tf[d->b_mn != 0], epi[gvl::gemm_w4_epi_kind(p)]);
     } else if (gvl::gemm_pp3_plan(p, cfg == 3 || cfg == 10)) {
-      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13"};
+      const char* epi[EPI_KINDS] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14"};
       const bool slab = p.splits > 1 && !(p.splits == 2 && p.tickets);  // partials-only kernel
       snprintf(buf, len, "gemm_pp3_kernel<4, %s, %s, %s, %d, %d>", tf[d->a_mn != 0], tf[d->b_mn != 0],
                epi[slab ? 0 : gvl::gemm_epi_kind(p)], p.bn, p.bm);
@@ -302,7 +302,9 @@ extern "C" int gvl_gemm(const gvl_gemm_desc* d, gvl_stream_t stream) {
               "gvl_gemm: leading dims must be multiples of 8 (lda, ldb) / 4 (ldc)");
   GVL_REQUIRE(gvl::aligned16(d->a) && gvl::aligned16(d->b) && gvl::aligned8(d->c),
               "gvl_gemm: operands must be 16-byte aligned");
-  GVL_REQUIRE(d->act >= 0 && d->act <= 4 && d->dact >= 0 && d->dact <= 3, "gvl_gemm: bad act");
+  GVL_REQUIRE(d->act >= 0 && d->act <= 5 && d->dact >= 0 && d->dact <= 3, "gvl_gemm: bad act");
+  GVL_REQUIRE(d->act != 5 || (d->pre_out == nullptr && d->dact == 0), "gvl_gemm: act 5 (quick-GELU) "
+              "has no pre-activation output and no dact");
   GVL_REQUIRE(!d->dact || (d->pre_in && d->ldp % 4 == 0), "gvl_gemm: dact needs pre_in");
   GVL_REQUIRE(!d->residual || d->ldr % 4 == 0, "gvl_gemm: ldr must be a multiple of 4");
   GVL_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "gvl_gemm: drop_p out of range");

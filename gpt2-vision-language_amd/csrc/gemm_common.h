@@ -150,7 +150,10 @@ static __device__ __forceinline__ void gemm_epi_vals(const GemmP& p, float4_t a,
       for (int r = 0; r < 4; ++r) v[r] *= h[r];
     }
   }
-  if (p.act) {
+  if (p.act == 5) {  // quick-GELU (no pre-activation output)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = quick_gelu(v[r]);
+  } else if (p.act) {
     float d[4];
     if (p.act == 1 || p.act == 2) {
       for (int r = 0; r < 4; ++r) d[r] = v[r];
@@ -205,9 +208,12 @@ enum {
   // the gate gradient: the cross-att decoder's xattn.c_proj (gpt2_cross-att/model.py:57,99-101).
   // Only the four-wave kernels take it (gemm_w4.hip, gemm_w4_epi_kind); gemm_epi_kind still
   // answers EPI_GEN for a gated GEMM, so no other kernel family sees this kind
-  EPI_GATE_RES = 13
+  EPI_GATE_RES = 13,
+  // C = quick_gelu(AB + bias) (act 5, no side output): the frozen CLIP ViT-L/14 MLP's fc1
+  // (transformers CLIPMLP, QuickGELUActivation) on the gvl-native feature stage (gvl/clip.py)
+  EPI_BIAS_QGELU = 14
 };
-constexpr int EPI_KINDS = 14;
+constexpr int EPI_KINDS = 15;
 
 template <int EPI>
 struct EpiKind {
@@ -218,7 +224,8 @@ struct EpiKind {
   static constexpr bool ERF = EPI == EPI_BIAS_ACT_ERF || EPI == EPI_DACT_ERF || EPI == EPI_BIAS_ACT_ERF_D;
   static constexpr bool DROP = EPI == EPI_BIAS_DROP_RES;
   static constexpr bool GATE = EPI == EPI_GATE_RES;
-  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT || DROP || GATE;
+  static constexpr bool QGELU = EPI == EPI_BIAS_QGELU;
+  static constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_RES || ACT || DROP || GATE || QGELU;
   static constexpr bool RES = EPI == EPI_BIAS_RES || EPI == EPI_RES || DROP || GATE;
   static constexpr bool PRE_OUT = ACT || GATE;  // stores a bf16 [M, N] side output (pre_out)
   static constexpr bool AUX = DACT || RES;  // reads a bf16 [M, N] operand (pre_in / residual)
@@ -287,6 +294,10 @@ static __device__ __forceinline__ void gemm_epi_vals_k(const GemmP& p, float4_t 
     for (int r = 0; r < 4; ++r) v[r] = a[r] * alpha;
     if constexpr (KD::BIAS) {
       v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+    }
+    if constexpr (KD::QGELU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = quick_gelu(v[r]);
     }
     if constexpr (KD::DACT) {
       const float h[4] = {lo_bf(ax.x), hi_bf(ax.x), lo_bf(ax.y), hi_bf(ax.y)};

@@ -22,6 +22,7 @@ int gemm_epi_kind(const GemmP& p) {
     if (b && r) return EPI_BIAS_RES;
     return EPI_RES;
   }
+  if (p.act == 5) return (!p.dact && b && !r && !p.pre_out) ? EPI_BIAS_QGELU : EPI_GEN;
   if (p.act && !p.dact && b && !r) {
     const int k[5] = {EPI_GEN, EPI_BIAS_ACT, EPI_BIAS_ACT_ERF, EPI_BIAS_ACT_D, EPI_BIAS_ACT_ERF_D};
     return k[p.act];

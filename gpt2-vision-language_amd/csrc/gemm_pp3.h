@@ -490,6 +490,7 @@ int launch_pp3_epi(const GemmP& p, hipStream_t s) {
     case EPI_BIAS_ACT_ERF_D: return launch_pp3<NS, AMN, BMN, EPI_BIAS_ACT_ERF_D>(p, s);
     case EPI_MUL: return launch_pp3<NS, AMN, BMN, EPI_MUL>(p, s);
     case EPI_BIAS_DROP_RES: return launch_pp3<NS, AMN, BMN, EPI_BIAS_DROP_RES>(p, s);
+    case EPI_BIAS_QGELU: return launch_pp3<NS, AMN, BMN, EPI_BIAS_QGELU>(p, s);
     default: return -1;  // EPI_GEN: gemm_pp3_plan never routes it here
   }
 }

@@ -584,7 +584,7 @@ int gemm_w4_epi_kind(const GemmP& p) {
 bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
   if (a_mn || p.c_f32 || p.K % (6 * KS) != 0 || p.N % 8 != 0 || p.ldc % 8 != 0) return false;
   if (p.pre_out && (p.ldp % 8 != 0 || (reinterpret_cast<uintptr_t>(p.pre_out) & 15))) return false;
-  if (gemm_w4_epi_kind(p) == EPI_GEN) return false;
+  if (gemm_w4_epi_kind(p) == EPI_GEN || gemm_w4_epi_kind(p) == EPI_BIAS_QGELU) return false;
   if (force || w4_mode() == 2) return true;
   if (w4_mode() == 0) return false;
   // GVL_W4=3 (A/B): also the short-K wide outputs (K <= 1024, N <= 4096: c_attn / c_fc

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVL_LIB", os.path.join(_HERE, "libgvl.so"))
-ABI_VERSION = 13  # include/gvl.h GVL_ABI_VERSION
+ABI_VERSION = 14  # include/gvl.h GVL_ABI_VERSION
 
 c_i64 = C.c_int64
 c_i32 = C.c_int32

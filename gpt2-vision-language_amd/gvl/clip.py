@@ -14,6 +14,17 @@ bias-free linear map, so pool(LN(h) @ P^T) == pool(LN(h)) @ P^T: the gvl pool ke
 the layer-normed 1024-d hidden states (no normalisation), the gvl GEMM projects only 33 of
 257 tokens (7.8x less projection work and no (B, 257, 768) intermediate), and
 gvl_l2_normalize_rows finishes.  `features(..., fused=False)` is the unfused composition.
+
+gvl-native tower (`CLIPFeatureStage(native=True)`, round 6; the stock tower stays the default,
+as the north star keeps CLIP on stock PyTorch-ROCm): the same frozen weights run through libgvl
+— per encoder layer LayerNorm -> ONE packed q|k|v GEMM (+ bias) -> the flash-attention forward
+(non-causal, 257 tokens, 16 heads of 64) reading q / k / v as strided views of it -> out_proj GEMM
+with bias + residual in its epilogue -> LayerNorm -> fc1 GEMM with bias + quick-GELU in its
+epilogue (ABI v14 act 5) -> fc2 GEMM with bias + residual.  The stock tower runs the same layer
+as separate q / k / v GEMMs, SDPA and five elementwise passes over the 32896 x 4096 fc1 output
+and the residual stream (quick-GELU as mul, sigmoid, mul; two residual adds):
+profiles/r6/clip_stock_kernel_table_r6g.txt.  Checked against the stock tower on the same
+weights (tests/test_gpu_models.py::test_clip_native_matches_stock).
 """
 from __future__ import annotations
 
@@ -32,10 +43,13 @@ FLOP_PER_IMAGE = 162e9  # ViT-L/14 forward at 224 px
 
 
 class CLIPFeatureStage(torch.nn.Module):
-    """Frozen ViT-L/14 vision tower + projection producing the caption models' inputs."""
+    """Frozen ViT-L/14 vision tower + projection producing the caption models' inputs.
+    native=True runs the tower's encoder on libgvl's kernels (module docstring)."""
 
-    def __init__(self, seed: int = 0, **over):
+    def __init__(self, seed: int = 0, native: bool = False, **over):
         super().__init__()
+        self.native = native
+        self._packed = None
         from transformers import CLIPVisionConfig, CLIPVisionModelWithProjection
         cfg = CLIPVisionConfig(**dict(VIT_L14, **over))
         cfg._attn_implementation = "sdpa"
@@ -53,8 +67,51 @@ class CLIPFeatureStage(torch.nn.Module):
         """Normalised pixels in [0, 1] (B, 3, 224, 224) -> layer-normed hidden (B, 257, 1024)."""
         vm = self.tower.vision_model
         x = ((pixels - self.mean) / self.std).to(next(self.tower.parameters()).dtype)
+        if self.native:
+            return self._native_hidden(vm, x)
         h = vm(pixel_values=x).last_hidden_state
         return vm.post_layernorm(h)
+
+    def _pack(self, vm):
+        """bf16 copies of the encoder weights in libgvl's layouts (q|k|v packed), built once."""
+        if self._packed is None:
+            bf = lambda t: t.detach().to(BF16).contiguous()  # noqa: E731
+            layers = []
+            for L in vm.encoder.layers:
+                a = L.self_attn
+                layers.append(dict(
+                    ln1=(bf(L.layer_norm1.weight), bf(L.layer_norm1.bias), L.layer_norm1.eps),
+                    wqkv=bf(torch.cat([a.q_proj.weight, a.k_proj.weight, a.v_proj.weight], 0)),
+                    bqkv=bf(torch.cat([a.q_proj.bias, a.k_proj.bias, a.v_proj.bias], 0)),
+                    wo=bf(a.out_proj.weight), bo=bf(a.out_proj.bias), heads=a.num_heads,
+                    scale=float(a.scale),
+                    ln2=(bf(L.layer_norm2.weight), bf(L.layer_norm2.bias), L.layer_norm2.eps),
+                    w1=bf(L.mlp.fc1.weight), b1=bf(L.mlp.fc1.bias),
+                    w2=bf(L.mlp.fc2.weight), b2=bf(L.mlp.fc2.bias)))
+            pre, post = vm.pre_layrnorm, vm.post_layernorm
+            self._packed = dict(layers=layers,
+                                pre=(bf(pre.weight), bf(pre.bias), pre.eps),
+                                post=(bf(post.weight), bf(post.bias), post.eps))
+        return self._packed
+
+    def _native_hidden(self, vm, x):
+        """The encoder on libgvl (module docstring): (B, 257, 1024) bf16, post-layernormed."""
+        P = self._pack(vm)
+        emb = vm.embeddings(pixel_values=x).to(BF16)  # conv patch embed + class + positions
+        B, T, C = emb.shape
+        h = K.layernorm_fwd(emb.reshape(B * T, C).contiguous(), *P["pre"][:2], eps=P["pre"][2],
+                            stats=False)[0]
+        for L in P["layers"]:
+            a = K.layernorm_fwd(h, *L["ln1"][:2], eps=L["ln1"][2], stats=False)[0]
+            qkv = K.gemm(a, L["wqkv"], bias=L["bqkv"]).view(B, T, 3 * C)
+            o, _ = K.attn_fwd(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], L["heads"], False,
+                              scale=L["scale"])
+            h = K.gemm(o.view(B * T, C), L["wo"], bias=L["bo"], residual=h)
+            a = K.layernorm_fwd(h, *L["ln2"][:2], eps=L["ln2"][2], stats=False)[0]
+            f = K.gemm(a, L["w1"], bias=L["b1"], act=5)  # fc1 + bias + quick-GELU
+            h = K.gemm(f, L["w2"], bias=L["b2"], residual=h)
+        h = K.layernorm_fwd(h, *P["post"][:2], eps=P["post"][2], stats=False)[0]
+        return h.view(B, T, C)
 
     @torch.no_grad()
     def tokens(self, pixels):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GVL_ABI_VERSION 13
+#define GVL_ABI_VERSION 14
 
 /* Dropout seeds: every dropout mask is rng(seed_eff, element index) with
  * seed_eff = seed when seed_ptr is NULL or *seed_ptr == 0, else seed ^ mix64(*seed_ptr).
@@ -67,7 +67,9 @@ typedef struct gvl_gemm_desc {
   const float* alpha_ptr; /* optional fp32 device scalar multiplied into alpha */
   const void* bias;       /* optional bf16 [N] */
   int32_t act;            /* 0 none, 1 gelu-tanh, 2 gelu-erf (pre_out <- x);
-                             3 gelu-tanh, 4 gelu-erf with pre_out <- gelu'(x) (ABI v4) */
+                             3 gelu-tanh, 4 gelu-erf with pre_out <- gelu'(x) (ABI v4);
+                             5 quick-GELU x sigmoid(1.702 x), needs bias, no pre_out, no dact
+                             (ABI v14: the frozen CLIP tower's fc1, gvl/clip.py) */
   int32_t dact;           /* 0 none, 1 dgelu-tanh, 2 dgelu-erf (of pre_in = x);
                              3: multiply by pre_in = gelu'(x) as stored by act 3/4 (ABI v4) */
   void* pre_out;          /* optional bf16 [M][ldp]: value before activation */

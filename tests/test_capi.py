@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     lib.gvl_abi_version.restype = ctypes.c_int
-    assert lib.gvl_abi_version() == 13
+    assert lib.gvl_abi_version() == 14
 
 
 def test_library_links_no_vendor_blas():
@@ -44,7 +44,7 @@ def test_binding_covers_header():
     from gvl import _lib
     assert sorted(_lib.SIGNATURES) == declared()
     lib = _lib.load()  # binds every symbol with its argtypes
-    assert lib.gvl_abi_version() == 13
+    assert lib.gvl_abi_version() == 14
 
 
 def test_rejects_bad_arguments_without_gpu():

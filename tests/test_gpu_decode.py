@@ -167,3 +167,31 @@ def test_clip_fused_pool_equals_unfused(cuda):
     norms = a.norm(dim=-1)
     print(f"fused vs unfused pool: rel err {err:.2e}; row norms {norms.min().item():.4f}..{norms.max().item():.4f}")
     assert err < 3e-2 and torch.allclose(norms, torch.ones_like(norms), atol=1e-2)
+
+
+def test_clip_native_matches_stock(cuda):
+    """gvl-native CLIP encoder (packed q|k|v GEMM, gvl flash attention, bias + residual and
+    bias + quick-GELU GEMM epilogues, gvl LayerNorm; gvl/clip.py) against the stock transformers
+    tower on the same frozen bf16 weights: the post-layernormed hidden states after 24 layers and
+    the pooled, normalised caption features.  Both sides compute in bf16 with different rounding
+    points (the stock quick-GELU rounds after each of its three ops), so the bound is a bf16
+    drift bound, recorded in parity_margins; the pooled features are the caption models' input."""
+    from gvl.clip import CLIPFeatureStage, synthetic_pixels
+    from tests.helpers import margins_out
+    clip = CLIPFeatureStage().to(cuda).to(BF)
+    px = synthetic_pixels(4, device=cuda)
+    hs = clip.hidden(px).float()
+    fs = clip.features(px).float()
+    clip.native = True
+    hn = clip.hidden(px).float()
+    fn = clip.features(px).float()
+    assert hn.shape == hs.shape == (4, 257, 1024)
+    h_rel = float((hn - hs).norm() / hs.norm())
+    f_rel = float((fn - fs).norm() / fs.norm())
+    cos = torch.nn.functional.cosine_similarity(fn.reshape(-1, 768), fs.reshape(-1, 768), dim=-1)
+    print(f"native vs stock CLIP: hidden rel-L2 {h_rel:.3e}, features rel-L2 {f_rel:.3e}, "
+          f"min cosine {cos.min().item():.5f}")
+    margins_out("clip_native_vs_stock", dict(hidden_rel_l2=h_rel, features_rel_l2=f_rel,
+                                             min_cosine=float(cos.min())))
+    assert torch.isfinite(hn).all()
+    assert h_rel < 5e-2 and f_rel < 3e-2 and float(cos.min()) > 0.999

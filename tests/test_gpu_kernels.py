@@ -152,8 +152,10 @@ def _kernel_name(A, B, a_mn, b_mn, M, N, K, tickets=False, epi=None):
     d.a_mn, d.b_mn = a_mn, b_mn
     d.alpha = 1.0
     p = A.data_ptr()  # any aligned device pointer: only the routing is asked
-    if epi in ("bias", "bias_res", "bias_act_d", "drop_res"):
+    if epi in ("bias", "bias_res", "bias_act_d", "drop_res", "qgelu"):
         d.bias = p
+    if epi == "qgelu":
+        d.act = 5
     if epi in ("bias_res", "res_inplace", "drop_res"):
         d.residual, d.ldr = p, N
     if epi == "bias_act_d":
@@ -1333,3 +1335,28 @@ def test_colsum_dropout_gate(cuda):
                                                   torch.zeros(1, device=cuda)).cpu())
         want_b = (torch.tensor(0.75).to(BF).float() + torch.tensor(wg).to(BF).float()).to(BF)
         assert abs(gb.float().item() - want_b.float().item()) <= 2 ** -7 * abs(want_b.float().item())
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 1024), (2056, 3072, 1024), (300, 136, 72)])
+def test_gemm_bias_quick_gelu(cuda, M, N, K):
+    """act 5 (ABI v14): C = quick_gelu(A W^T + b) = h * sigmoid(1.702 h), the frozen CLIP tower's
+    fc1 (transformers QuickGELUActivation) on the gvl-native feature stage — the persistent
+    kernel's compile-time epilogue (EPI_BIAS_QGELU) on the wide shapes, the generic epilogue on a
+    ragged small one; quick-GELU with a pre-activation output is refused."""
+    K_ = _k()
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(N, K) * 0.05).to(BF)
+    bias = torch.randn(N).to(BF)
+    A, B = x.to(cuda), w.to(cuda)
+    name = _kernel_name(A, B, 0, 0, M, N, K, epi="qgelu")
+    y = K_.gemm(A, B, bias=bias.to(cuda), act=5)
+    torch.cuda.synchronize()
+    h = x.float() @ w.float().t() + bias.float()
+    ref = h * torch.sigmoid(1.702 * h)
+    print(name)
+    if M == 4096:  # (2056 rows: too few tiles for the persistent kernel, the ring's generic epilogue)
+        assert name.startswith("gemm_pp3_kernel") and ", 14, " in name, name
+    assert rel_err(y.float().cpu().numpy(), ref.numpy()) < 8e-3
+    with pytest.raises(RuntimeError):
+        K_.gemm(A, B, bias=bias.to(cuda), act=5, pre_out=torch.empty(M, N, dtype=BF, device=cuda))

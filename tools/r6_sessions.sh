@@ -105,5 +105,38 @@ r6pmc|r6pmc2)  # PMC passes (FETCH / WRITE / MFMA busy + clock) of all four benc
   timeout -k 10 1100 bash tools/pmc_traffic.sh $S "lm qf cross linear"; fatal $? pmc
   python -c "import json;d=json.load(open('gpurun_out/pmc_traffic_$S.json'));[print(w, k, v['hbm_bytes'], v.get('mfma_busy'), v.get('clock_ghz')) for w in d['workloads'] for k, v in list(d['workloads'][w].items())[:2]]"
   ;;
+r6f)  # short attention backward: memory floor of its access pattern (timing-only libgvl_sdiag.so:
+      # the loads, then the stores of the same bytes) vs the shipped kernel. Bound: if the floor is
+      # near the kernel's 23 us, the kernel is paced by its 99 MB at ~4 TB/s and only the access
+      # pattern can move it (2-4 % of the caption steps)
+  for r in 1 2; do for L in base sdiag; do
+    LIB=$LIBDIR/libgvl.so; [ $L != base ] && LIB=$LIBDIR/libgvl_$L.so
+    GVL_LIB=$LIB timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_${L}_$r.log 2>&1; fatal $? attn
+    echo "attn $L $r"; grep -E "Tq=63|Tq=31|Tq=32 Tk=32" $O/attn_${L}_$r.log
+  done; done
+  ;;
+r6g)  # frozen CLIP ViT-L/14 stage (configs[3] pixel input; stock PyTorch-ROCm): where its ~38 ms per
+      # B = 128 go. Bound: it is ~85 % of the caption_linear_pixels step at ~0.22 of the bf16 peak
+  timeout -k 10 300 python -u tools/clip_prof.py 128 10 eager > $O/clip_eager.log 2>&1; fatal $? clip; cat $O/clip_eager.log | grep CLIP
+  timeout -k 10 300 python -u tools/clip_prof.py 128 10 graph > $O/clip_graph.log 2>&1; fatal $? clip_graph; cat $O/clip_graph.log | grep CLIP
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_clip -o clip -- \
+    python tools/clip_prof.py 128 5 eager > $O/prof_clip.log 2>&1; fatal $? prof_clip
+  f=$(find $O/prof_clip -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 30 > $O/clip_table.txt; cat $O/clip_table.txt
+  ;;
+r6h)  # gvl-native CLIP encoder (configs[3] pixel input) + the quick-GELU epilogue (ABI v14). Bound: the
+      # stock tower's 38.5 ms per B = 128 spends ~12 ms in elementwise / LayerNorm passes and 4.6 ms in
+      # SDPA around 21.7 ms of GEMMs at ~0.38: fused epilogues + gvl attention/LN -> ~22-25 ms
+  ktests kt "gemm or quick_gelu"
+  ktests capi "" tests/test_capi.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests clip "clip" tests/test_gpu_decode.py
+  for m in eager native native_graph; do
+    timeout -k 10 300 python -u tools/clip_prof.py 128 10 $m > $O/clip_$m.log 2>&1; fatal $? clip_$m; grep CLIP $O/clip_$m.log
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_clipn -o clipn -- \
+    python tools/clip_prof.py 128 5 native > $O/prof_clipn.log 2>&1; fatal $? prof_clipn
+  f=$(find $O/prof_clipn -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 25 > $O/clipn_table.txt; cat $O/clipn_table.txt
+  timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err; fatal $? bench
+  python -c "import json;d=json.load(open('$O/bench.json'));p=d['caption_linear_pixels'];print('pixels stock',p['value'],p['clip_ms_per_batch'],'native',p['native_clip'])"
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
