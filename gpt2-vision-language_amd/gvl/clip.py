@@ -94,6 +94,23 @@ class CLIPFeatureStage(torch.nn.Module):
                                 post=(bf(post.weight), bf(post.bias), post.eps))
         return self._packed
 
+    @staticmethod
+    def _gemm(a, w, bias, residual=None, act=0):
+        """A W^T + bias (+ residual / quick-GELU) over the B x 257 token rows, as two launches: the
+        first 256 x floor(M / 256) rows and the tail.  32896 rows are 128.5 row blocks of 256: one
+        launch would run out_proj / fc2 (N = 1024) as 516 tiles of 256 x 256 = 2.02 rounds of 256
+        CUs (a third round for 4 tiles), the q|k|v and fc1 GEMMs as 6.05 / 8.06 rounds; split, the
+        bulk is exactly 2 / 6 / 8 rounds and the 128-row tail a small launch of its own."""
+        M = a.shape[0]
+        Mb = M // 256 * 256
+        if Mb == M or Mb == 0:
+            return K.gemm(a, w, bias=bias, residual=residual, act=act)
+        out = torch.empty(M, w.shape[0], dtype=BF16, device=a.device)
+        for r0, r1 in ((0, Mb), (Mb, M)):
+            K.gemm(a[r0:r1], w, bias=bias, act=act, out=out[r0:r1],
+                   residual=None if residual is None else residual[r0:r1])
+        return out
+
     def _native_hidden(self, vm, x):
         """The encoder on libgvl (module docstring): (B, 257, 1024) bf16, post-layernormed."""
         P = self._pack(vm)
@@ -103,13 +120,13 @@ class CLIPFeatureStage(torch.nn.Module):
                             stats=False)[0]
         for L in P["layers"]:
             a = K.layernorm_fwd(h, *L["ln1"][:2], eps=L["ln1"][2], stats=False)[0]
-            qkv = K.gemm(a, L["wqkv"], bias=L["bqkv"]).view(B, T, 3 * C)
+            qkv = self._gemm(a, L["wqkv"], L["bqkv"]).view(B, T, 3 * C)
             o, _ = K.attn_fwd(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], L["heads"], False,
                               scale=L["scale"])
-            h = K.gemm(o.view(B * T, C), L["wo"], bias=L["bo"], residual=h)
+            h = self._gemm(o.view(B * T, C), L["wo"], L["bo"], residual=h)
             a = K.layernorm_fwd(h, *L["ln2"][:2], eps=L["ln2"][2], stats=False)[0]
-            f = K.gemm(a, L["w1"], bias=L["b1"], act=5)  # fc1 + bias + quick-GELU
-            h = K.gemm(f, L["w2"], bias=L["b2"], residual=h)
+            f = self._gemm(a, L["w1"], L["b1"], act=5)  # fc1 + bias + quick-GELU
+            h = self._gemm(f, L["w2"], L["b2"], residual=h)
         h = K.layernorm_fwd(h, *P["post"][:2], eps=P["post"][2], stats=False)[0]
         return h.view(B, T, C)
 

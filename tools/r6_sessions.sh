@@ -138,5 +138,16 @@ r6h)  # gvl-native CLIP encoder (configs[3] pixel input) + the quick-GELU epilog
   timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err; fatal $? bench
   python -c "import json;d=json.load(open('$O/bench.json'));p=d['caption_linear_pixels'];print('pixels stock',p['value'],p['clip_ms_per_batch'],'native',p['native_clip'])"
   ;;
+r6i)  # native CLIP GEMMs split at 256 x floor(M / 256) rows (whole CU rounds). Bound: out_proj / fc2 run
+      # 3 rounds for 2.02 rounds of tiles (12.7 ms of the 29 ms forward) -> ~4 ms off
+  GVL_MARGINS_DIR=$O/parity_margins ktests clip "clip" tests/test_gpu_decode.py
+  cat $O/parity_margins/clip_native_vs_stock.json
+  for m in native eager native; do
+    timeout -k 10 300 python -u tools/clip_prof.py 128 10 $m > $O/clip_$m.log 2>&1; fatal $? clip_$m; grep CLIP $O/clip_$m.log
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_clipn -o clipn -- \
+    python tools/clip_prof.py 128 5 native > $O/prof_clipn.log 2>&1; fatal $? prof_clipn
+  f=$(find $O/prof_clipn -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 25 > $O/clipn_table.txt; head -14 $O/clipn_table.txt
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
