@@ -261,7 +261,8 @@ extern "C" int gvl_gemm_kernel_name(const gvl_gemm_desc* d, char* buf, int32_t l
                  tf[d->b_mn != 0], epi[gvl::gemm_epi_kind(p)]);
       else
         snprintf(buf, len, "%s<3, %s, %s>",
-                 gvl::gemm_w4_cols96(p, d->b_mn != 0) ? "gemm_w4n_kernel"
+                 gvl::gemm_w4_rows96(p, d->b_mn != 0) ? "gemm_w4r_kernel"
+                 : gvl::gemm_w4_cols96(p, d->b_mn != 0) ? "gemm_w4n_kernel"
                  : gvl::gemm_w4_rows128(p) ? "gemm_w4m_kernel" : "gemm_w4_kernel",
                  tf[d->b_mn != 0], epi[gvl::gemm_w4_epi_kind(p)]);
     } else if (gvl::gemm_pp3_plan(p, cfg == 3 || cfg == 10)) {

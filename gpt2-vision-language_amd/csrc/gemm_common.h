@@ -545,6 +545,7 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force);  // gemm_w4.hip
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s);
 bool gemm_w4_rows128(const GemmP& p);  // the launch uses 128-row tiles (gemm_w4m_kernel)
 bool gemm_w4_cols96(const GemmP& p, bool b_mn);  // ... and 96-column ones (gemm_w4n_kernel)
+bool gemm_w4_rows96(const GemmP& p, bool b_mn);  // 96 x 128 dX tiles (gemm_w4r_kernel)
 int gemm_w4_epi_kind(const GemmP& p);  // gemm_epi_kind + EPI_GATE_RES (four-wave kernels only)
 bool gemm_w4_try(const GemmP& p, int a_mn, int b_mn, hipStream_t s);
 bool gemm_w4d_ok(const GemmP& p);  // gemm_w4d.hip: direct-A variant for a w4-planned shape

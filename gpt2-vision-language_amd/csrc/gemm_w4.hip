@@ -116,6 +116,15 @@ template <bool MN>
 struct W4SlabB<96, MN> {
   using type = Step96<MN>;
 };
+// A slab (K-contiguous): the Step image, or Step96's [96 rows][32] one for 96-row tiles
+template <int BM>
+struct W4SlabA {
+  using type = Step<BM, false, 4>;
+};
+template <>
+struct W4SlabA<96> {
+  using type = Step96<false>;
+};
 
 // K-steps are 32 deep; the register staging runs P = 3 steps ahead of the LDS writes, the LDS
 // ring holds NS = 3 steps (the one being read, the next, the one being written).  Step c:
@@ -212,9 +221,9 @@ template <int NS, bool BMN, int EPI, int BM, int BN = W4_BN>
 __device__ __forceinline__ void gemm_w4_body(const GemmP& p) {
   constexpr int NW = 4, FM = BM / 32, FN = BN / 32, P = 3;
   static_assert(NS == 3, "ring geometry");
-  static_assert(BM == 192 || BM == 128, "tile rows");
+  static_assert(BM == 192 || BM == 128 || (BM == 96 && BN == 128), "tile rows");
   static_assert(BN == 128 || (BN == 96 && BM == 128), "tile columns");
-  using SA = Step<BM, false, NW>;
+  using SA = typename W4SlabA<BM>::type;
   using SB = typename W4SlabB<BN, BMN>::type;
   constexpr int SLOT = SA::BYTES + SB::BYTES;
   constexpr int PA = SA::PER, PB = SB::PER;
@@ -451,6 +460,10 @@ template <int NS, bool BMN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4n_kernel(GemmP p) {
   gemm_w4_body<NS, BMN, EPI, 128, 96>(p);
 }
+template <int NS, bool BMN, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(GemmP p) {
+  gemm_w4_body<NS, BMN, EPI, 96, 128>(p);
+}
 
 #ifndef GVL_W4_NS
 #define GVL_W4_NS 3
@@ -467,6 +480,15 @@ int w4_group(int dflt) {
   return g > 0 ? g : dflt;
 }
 
+// the kernel of a tile shape (if constexpr: only the chosen one is instantiated)
+template <int BM, int BN, bool BMN, int EPI>
+constexpr auto w4_kernel_of() {
+  if constexpr (BN == 96) return gemm_w4n_kernel<GVL_W4_NS, BMN, EPI>;
+  else if constexpr (BM == 96) return gemm_w4r_kernel<GVL_W4_NS, BMN, EPI>;
+  else if constexpr (BM == 192) return gemm_w4_kernel<GVL_W4_NS, BMN, EPI>;
+  else return gemm_w4m_kernel<GVL_W4_NS, BMN, EPI>;
+}
+
 template <bool BMN, int EPI, int BM, int BN = W4_BN>
 int launch_w4_bm(const GemmP& p0, hipStream_t s) {
   constexpr int NS = GVL_W4_NS;
@@ -476,10 +498,9 @@ int launch_w4_bm(const GemmP& p0, hipStream_t s) {
   p.splits = 1;
   p.kper = p.K;
   p.group = w4_group(p.group);
-  constexpr int slot = BM * KS * 2 + W4SlabB<BN, BMN>::type::BYTES;
+  constexpr int slot = W4SlabA<BM>::type::BYTES + W4SlabB<BN, BMN>::type::BYTES;
   constexpr int lds = NS * slot;
-  auto kern = BN == 96 ? gemm_w4n_kernel<GVL_W4_NS, BMN, EPI>
-              : BM == 192 ? gemm_w4_kernel<GVL_W4_NS, BMN, EPI> : gemm_w4m_kernel<GVL_W4_NS, BMN, EPI>;
+  auto kern = w4_kernel_of<BM, BN, BMN, EPI>();
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -524,8 +545,27 @@ bool w4_use96(const GemmP& p, bool b_mn) {
   return t96 > t128 && t96 <= cus;
 }
 
+// 96 x 128 tiles (gemm_w4r_kernel) for the dX products (MN-contiguous weight, plain epilogue)
+// where 128-row tiles are used and 96-row ones fill more of the chip in one round: the cross-att
+// decoder's 3968 text rows, 186 -> 252 tiles at N = 768.  The 128-column B image keeps its full
+// 256-B rows (the 96-column one of gemm_w4n_kernel lost on dX: 64-B row segments); the A slab is
+// Step96's [96][32] image (two dummy pieces).  GVL_W4_BM96=0: off (A/B).
+bool w4_use96r(const GemmP& p, bool b_mn) {
+  static const bool on = [] {
+    const char* e = getenv("GVL_W4_BM96");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !b_mn || !w4_use128(p)) return false;
+  const int64_t cus = gvl::num_cus(), tn = (p.N + 127) / 128;
+  const int64_t t128 = (p.M + 127) / 128 * tn, t96 = (p.M + 95) / 96 * tn;
+  return t96 > t128 && t96 <= cus;
+}
+
 template <bool BMN, int EPI>
 int launch_w4(const GemmP& p, hipStream_t s) {
+  if constexpr (BMN && EPI == EPI_PLAIN) {
+    if (w4_use96r(p, BMN)) return launch_w4_bm<BMN, EPI, 96, 128>(p, s);
+  }
   if (w4_use96(p, BMN)) return launch_w4_bm<BMN, EPI, 128, 96>(p, s);
   return w4_use128(p) ? launch_w4_bm<BMN, EPI, 128>(p, s) : launch_w4_bm<BMN, EPI, 192>(p, s);
 }
@@ -605,6 +645,9 @@ bool gemm_w4_plan(const GemmP& p, int a_mn, bool force) {
 
 bool gemm_w4_rows128(const GemmP& p) { return w4_use128(p); }
 bool gemm_w4_cols96(const GemmP& p, bool b_mn) { return w4_use96(p, b_mn); }
+bool gemm_w4_rows96(const GemmP& p, bool b_mn) {
+  return gemm_w4_epi_kind(p) == EPI_PLAIN && w4_use96r(p, b_mn);
+}
 
 int gemm_w4_launch(const GemmP& p, int b_mn, hipStream_t s) {
   if (gemm_w4d_ok(p)) {

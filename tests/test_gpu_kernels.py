@@ -548,6 +548,16 @@ def _w4_tiles(M, N, b_mn=0, cus=256):
     return r128, c96
 
 
+def _w4_rows96(M, N, b_mn, epi, cus=256):
+    """96 x 128 dX tiles (gemm_w4r_kernel) as gemm_w4.hip's w4_use96r decides: MN-contiguous B,
+    plain epilogue, 128-row tiles in use and 96-row ones filling more of the chip in one round."""
+    r128, _ = _w4_tiles(M, N, b_mn, cus)
+    tn = -(-N // 128)
+    t128, t96 = -(-M // 128) * tn, -(-M // 96) * tn
+    return (r128 and b_mn and epi == "plain" and os.environ.get("GVL_W4_BM96", "1") != "0"
+            and t128 < t96 <= cus)
+
+
 def _w4_name(M, K, epi, N=768, b_mn=0):
     """Kernel the default four-wave routing picks (GVL_W4D unset): the direct-A variant
     (gemm_w4d.h) when K is a multiple of six 64-deep steps and the epilogue is one of its;
@@ -559,6 +569,8 @@ def _w4_name(M, K, epi, N=768, b_mn=0):
     direct = K % 384 == 0 and epi in W4D_EPIS and mode != "0" and (mode == "2" or not rows)
     if direct:
         return f"gemm_w4d{rows}_kernel"
+    if _w4_rows96(M, N, b_mn, epi):
+        return "gemm_w4r_kernel"
     return "gemm_w4n_kernel" if c96 else f"gemm_w4{rows}_kernel"
 
 

@@ -149,5 +149,25 @@ r6i)  # native CLIP GEMMs split at 256 x floor(M / 256) rows (whole CU rounds). 
     python tools/clip_prof.py 128 5 native > $O/prof_clipn.log 2>&1; fatal $? prof_clipn
   f=$(find $O/prof_clipn -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 25 > $O/clipn_table.txt; head -14 $O/clipn_table.txt
   ;;
+r6j)  # native CLIP attention at T = 257 with 64-row query blocks (GVL_ATTN_G=1) vs 128-row (default G = 2:
+      # 257 = 2 x 128 + 1, the third block of every (b, h) holds one query row). Bound: 2.7 ms of 24.8
+  for r in 1 2; do for g in 0 1; do
+    if [ $g = 1 ]; then export GVL_ATTN_G=1; else unset GVL_ATTN_G; fi
+    timeout -k 10 300 python -u tools/clip_prof.py 128 10 native > $O/clip_g${g}_$r.log 2>&1; fatal $? clip; echo "G1=$g $(grep CLIP $O/clip_g${g}_$r.log)"
+  done; done
+  unset GVL_ATTN_G
+  ;;
+r6k)  # 96 x 128 dX tiles (gemm_w4r_kernel) for the cross-att decoder's 3968-row N = 768 dX products.
+      # Bound: gemm_w4m_kernel<3, true, 0> is 18.9 % of the cross step at 186 tiles, one round;
+      # 252 tiles streaming 224 instead of 256 rows each -> ~12 % off = ~2.3 % of the step
+  ktests kt "test_gemm_w4 or gated or caption_dx or tile128x192"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "cross" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "cross" tests/test_gpu_parity_full.py
+  for v in 1 0; do
+    GVL_W4_BM96=$v GVL_DIAG_COLS=epi timeout -k 10 240 python -u tools/gemm_diag.py 3968 narrow > $O/diag_bm96_${v}.log 2>&1; fatal $? diag
+    echo "== 3968 BM96=$v"; grep "N=" $O/diag_bm96_${v}.log
+  done
+  for r in 1 2; do for v in 1 0; do GVL_W4_BM96=$v bench cross_r${v}_$r cross; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
