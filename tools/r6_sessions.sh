@@ -169,5 +169,13 @@ r6k)  # 96 x 128 dX tiles (gemm_w4r_kernel) for the cross-att decoder's 3968-row
   done
   for r in 1 2; do for v in 1 0; do GVL_W4_BM96=$v bench cross_r${v}_$r cross; done; done
   ;;
+r6l)  # c_attn forward split into q (N = 768, four-wave kernels) + k|v (N = 1536, 256 tiles) at the caption
+      # decoders' 8064 / 8192 rows (GVL_QKV_SPLIT=1) vs one 384-tile GEMM (1.5 rounds). Bound: pp3 1 is
+      # 8.0 % of the Q-Former and 8.8 % of the linear step; one round each -> ~20 % off = ~1.6-2 %
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or linear or lm" tests/test_gpu_parity_bench.py
+  GVL_MARGINS_DIR=$O/parity_margins ktests full "" tests/test_gpu_parity_full.py
+  ktests models "" tests/test_gpu_models.py
+  for r in 1 2; do for v in 1 0; do GVL_QKV_SPLIT=$v bench qf_s${v}_$r qformer; GVL_QKV_SPLIT=$v bench lin_s${v}_$r linear; done; done
+  ;;
 *) echo "unknown session $S"; exit 2 ;;
 esac
