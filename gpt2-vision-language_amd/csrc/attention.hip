@@ -50,7 +50,8 @@ struct AttnG {
   bf16_t* dq; int64_t dq_sb, dq_st, dq_sh;
   bf16_t* dk; int64_t dk_sb, dk_st, dk_sh;
   bf16_t* dv; int64_t dv_sb, dv_st, dv_sh;
-  float* Dws;
+  float* Dws;  // D = rowsum(dO * O) per query row, written by the dQ kernel
+  float* Lws;  // lse * log2(e) per query row (ditto): the dK/dV kernel's exp2 argument as is
 };
 
 // 1-D grid, heavy tiles first: the block id's slowest digit is the tile index, so every
@@ -414,6 +415,27 @@ GVL_DEV short8_t frag_tr_asm(const char* lds, int t, int s, int lane) {
   r.hi = hi;
   return r;
 }
+// The same fragment from a per-lane address register and instruction offsets.  In frag_tr's
+// layout only the lane picks the swizzled chunk ((row >> 1) & 3 is the same for rows ra,
+// ra + 16 and ra + 32 s), so a tile's transposed reads need one address register per column
+// block t (tr_lane) and the k-half / second row group are offsets (+4096 s, +2048).
+// frag_tr_asm took two fully computed addresses per read: hipcc spent a v_add_u32 on each, 64 per
+// dK/dV query tile (a quarter of that loop's vector issue cycles) and 16-32 per forward / dQ key tile.
+GVL_DEV uint32_t tr_lane(const char* lds, int t, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  return (uint32_t)reinterpret_cast<uintptr_t>(lds) + swz_tr(4 * G + q, 2 * t + (p >> 1)) + (p & 1) * 8;
+}
+template <int OFF>  // tile offset + 4096 s (< 65536 - 2048: the ds offset field)
+GVL_DEV short8_t frag_tr_imm(uint32_t a) {
+  static_assert(OFF >= 0 && OFF + 2048 < 65536, "ds offset");
+  short4_t lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+               : "=&v"(lo), "=&v"(hi) : "v"(a), "n"(OFF), "n"(OFF + 2048) : "memory");
+  short8_t r;
+  r.lo = lo;
+  r.hi = hi;
+  return r;
+}
 // lgkmcnt(N) with the fragments threaded through: all but this wave's N newest LDS operations
 // done (LDS operations complete in order, so the fragments read before the N newest are in)
 template <int N>
@@ -447,10 +469,11 @@ GVL_DEV void frags_landed(short8_t (&a)[G][2], short8_t (&b)[G][2]) {
 // lds_wait_pair<N> waits until at most N of this wave's LDS operations are in flight, with the
 // pair threaded through so no use is scheduled above the wait.  Early-clobber: a result must not
 // land on the address register of the second read.
-GVL_DEV void lds_pair(float4_t& l4, float4_t& d4, const float* a) {
-  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:256"
+template <int OFF>  // byte offset of the fragment row from a (one address register per tile)
+GVL_DEV void lds_pair(float4_t& l4, float4_t& d4, uint32_t a) {
+  asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4"
                : "=&v"(l4), "=&v"(d4)
-               : "v"((uint32_t)reinterpret_cast<uintptr_t>(a))
+               : "v"(a), "n"(OFF), "n"(OFF + 256)
                : "memory");
 }
 template <int N>
@@ -505,7 +528,7 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
   // buffer resources (bounds = the last valid row's end: rows >= Tq read zero)
   const __amdgpu_buffer_rsrc_t rq = gvl_ring::uniform_rsrc(qbase, ((p.Tq - 1) * p.q_st + D) * 2);
   const __amdgpu_buffer_rsrc_t rd = gvl_ring::uniform_rsrc(dobase, ((p.Tq - 1) * gg.do_st + D) * 2);
-  const __amdgpu_buffer_rsrc_t rl = gvl_ring::uniform_rsrc(p.lse + rbase, p.Tq * 4);
+  const __amdgpu_buffer_rsrc_t rl = gvl_ring::uniform_rsrc(gg.Lws + rbase, p.Tq * 4);
   const __amdgpu_buffer_rsrc_t rD = gvl_ring::uniform_rsrc(gg.Dws + rbase, p.Tq * 4);
   // DMA instructions per wave per tile: 4 (+1 for waves 0 / 1: the lse / D row).  Wave w
   // issues pieces 2w, 2w+1 (rows 8j .. 8j+7) of each tile; the lane offsets include the tile
@@ -562,7 +585,11 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
     constexpr bool MASK = decltype(mtag)::value;
     const int qt = qt_first + i, st = i % 3;
     if (i + 2 < nq) issue(qt + 2, (i + 2) % 3);
-    const char* qs = smem + st * DK_SLOT;
+    // the slot offset opaque to hipcc: otherwise it strength-reduces the slot addresses into an
+    // induction pointer past the slot and every row read needs its own v_add (negative offsets)
+    int soff = __builtin_amdgcn_readfirstlane(st * DK_SLOT);
+    asm volatile("" : "+s"(soff));
+    const char* qs = smem + soff;
     const char* ds = qs + KT * D * 2;
     const float* sl = reinterpret_cast<const float*>(qs + 2 * KT * D * 2);
     const int64_t q0 = (int64_t)qt * KT;
@@ -599,11 +626,14 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
       // leaves it in flight (round 4 waited for each pair with lgkmcnt(0): four exposed LDS round
       // trips per query tile; PMC r5d: waves parked 37 % of their cycles)
       float4_t lv[2], dv2[2];
-      lds_pair(lv[0], dv2[0], sl + 4 * Gl);
+      const uint32_t sla = (uint32_t)reinterpret_cast<uintptr_t>(sl + 4 * Gl);
+      lds_pair<0>(lv[0], dv2[0], sla);
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
+        if (n == 0) lds_pair<64>(lv[1], dv2[1], sla);
+        if (n == 1) lds_pair<128>(lv[0], dv2[0], sla);
+        if (n == 2) lds_pair<192>(lv[1], dv2[1], sla);
         if (n < 3) {
-          lds_pair(lv[(n + 1) & 1], dv2[(n + 1) & 1], sl + 16 * (n + 1) + 4 * Gl);
           lds_wait_pair<2>(lv[n & 1], dv2[n & 1]);
         } else {
           lds_wait_pair<0>(lv[n & 1], dv2[n & 1]);
@@ -612,7 +642,7 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = 16 * n + 4 * Gl + r;
-          const float lr = l4[r] * LOG2E;
+          const float lr = l4[r];  // lse * log2(e) (Lws)
           const float dr = d4[r];
           float pv = __builtin_amdgcn_exp2f(fmaf(sc[g][n][r], p.c2, -lr));
           if (msk && (!kok[g] || qi >= qlim || (p.causal && kq > qi))) pv = 0.f;
@@ -632,13 +662,16 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
       sf[g][0] = pack_frag(sc[g][0], sc[g][1]);
       sf[g][1] = pack_frag(sc[g][2], sc[g][3]);
     }
+    uint32_t ta[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int t = 0; t < 4; ++t) ta[t] = tr_lane(qs, t, lane);
+    auto half = [&](auto s2c) __attribute__((always_inline)) {
+      constexpr int s2 = decltype(s2c)::value;
       short8_t dof[4], qtf[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        dof[t] = frag_tr_asm(ds, t, s2, lane);
-        qtf[t] = frag_tr_asm(qs, t, s2, lane);
+        dof[t] = frag_tr_imm<KT * D * 2 + 4096 * s2>(ta[t]);
+        qtf[t] = frag_tr_imm<4096 * s2>(ta[t]);
       }
       lds_wait8(dof, qtf);
 #pragma unroll
@@ -648,7 +681,9 @@ __global__ __launch_bounds__(NT, G == 1 ? 3 : 2) void attn_bwd_dkdv_dma_kernel(A
           dv[g][t] = mfma16(dof[t], pf[g][s2], dv[g][t]);
           dk[g][t] = mfma16(qtf[t], sf[g][s2], dk[g][t]);
         }
-    }
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
     if (i + 1 < nq) wait_tiles(i + 2 < nq ? 1 : 0);
     gvl_ring::barrier_lds();  // slot st is refilled by iteration i+1's issue
     };
@@ -832,11 +867,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
     }
     // K^T fragments of both k-halves issued before the first half's MFMAs (+16 VGPRs; the
     // kernel is at 2 waves per SIMD either way)
+    // (issue order: the k-half 0 reads first — lds_wait_n<8> below counts on it)
     short8_t kta[2][4];
+    uint32_t ta[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+    for (int t = 0; t < 4; ++t) ta[t] = tr_lane(ks, t, lane);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) kta[s2][t] = frag_tr_asm(ks, t, s2, lane);
+    for (int t = 0; t < 4; ++t) kta[0][t] = frag_tr_imm<0>(ta[t]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kta[1][t] = frag_tr_imm<4096>(ta[t]);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       short8_t (&kt4)[4] = kta[s2];
@@ -858,7 +897,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_dma_kernel(AttnP p, AttnG g
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (!qok[g]) continue;
-    if (Gl == 0) gg.Dws[(b * p.H + h) * p.Tq + q[g]] = Dq[g];  // read by the dK/dV kernel
+    if (Gl == 0) {  // read by the dK/dV kernel
+      gg.Dws[(b * p.H + h) * p.Tq + q[g]] = Dq[g];
+      gg.Lws[(b * p.H + h) * p.Tq + q[g]] = lse2[g];
+    }
     bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + q[g] * gg.dq_st;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -958,8 +1000,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
   auto tile = [&](int kt, auto mtag) __attribute__((always_inline)) {
     constexpr bool MASK = decltype(mtag)::value;
     if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
-    const char* ks = smem + (kt % 3) * SLOT;
-    const char* vs = ks + KT * D * 2;
+    const char* ks = smem + (kt % 3) * SLOT;  // V: the tile at + KT * D * 2
     const int64_t k0 = (int64_t)kt * KT;
     float4_t sc[G][4];
 #pragma unroll
@@ -1016,11 +1057,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
     }
     // V fragments of both k-halves issued before the first half's MFMAs (the second half's
     // LDS latency hides behind them; +16 VGPRs, still 3 waves per SIMD)
+    // (issue order: the k-half 0 reads first — lds_wait_n<8> below counts on it)
     short8_t vfa[2][4];
+    uint32_t ta[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+    for (int t = 0; t < 4; ++t) ta[t] = tr_lane(ks, t, lane);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) vfa[s2][t] = frag_tr_asm(vs, t, s2, lane);
+    for (int t = 0; t < 4; ++t) vfa[0][t] = frag_tr_imm<KT * D * 2>(ta[t]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) vfa[1][t] = frag_tr_imm<KT * D * 2 + 4096>(ta[t]);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       short8_t (&vf)[4] = vfa[s2];
@@ -1370,7 +1415,7 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
 }
 
 extern "C" int64_t gvl_attn_bwd_workspace_size(const gvl_attn_desc* d) {
-  return d->B * d->H * d->Tq * (int64_t)sizeof(float);
+  return 2 * d->B * d->H * d->Tq * (int64_t)sizeof(float);  // Dws, Lws
 }
 
 extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
@@ -1392,6 +1437,7 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   g.dv = static_cast<bf16_t*>(gd->dv);
   g.dv_sb = gd->dv_sb; g.dv_st = gd->dv_st; g.dv_sh = gd->dv_sh;
   g.Dws = static_cast<float*>(gd->workspace);
+  g.Lws = g.Dws + d->B * d->H * d->Tq;
   hipStream_t s = gvl::as_stream(stream);
   if (d->Tq <= 64 && d->Tk <= 64 && short_bwd_enabled()) {
     dim3 grid((unsigned)(d->B * d->H));

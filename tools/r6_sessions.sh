@@ -24,6 +24,24 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6m)  # attention address registers (tr_lane / frag_tr_imm: one VGPR per column block, the k-half
+      # and row group as ds offsets; dK/dV slot offset opaque). Bound: ISA count per dK/dV query
+      # tile 64 -> 12 v_add_u32 (of ~250 vector issues), forward / dQ key tile 29 -> 13; attention
+      # is 14.2 % of the LM step, dK/dV 7.8 % -> if issue-bound ~15-20 % off dK/dV, ~5 % off fwd / dQ:
+      # LM +1.5-2 %. Base = the same tree with HEAD's attention.hip (libgvl_base.so).
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm" tests/test_gpu_parity_bench.py
+  ktests full "lm or accumulation" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in base new; do
+    L=$LIBDIR/libgvl.so; [ $v = base ] && L=$LIBDIR/libgvl_base.so
+    GVL_LIB=$L timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_${v}_$r.log 2>&1; fatal $? attn_$v
+    echo "== attn $v $r"; grep -v amdgpu.ids $O/attn_${v}_$r.log | head -8
+  done; done
+  for r in 1 2; do for v in base new; do
+    L=$LIBDIR/libgvl.so; [ $v = base ] && L=$LIBDIR/libgvl_base.so
+    GVL_LIB=$L bench lm_${v}_$r lm
+  done; done
+  ;;
 r6a)  # teardown (GraphedStep.close, gvl.dist.destroy_process_group) tests; two-stream overlap probe
       # (bound for the Q-Former two-branch lever: up to the 20 % non-GEMM share if half-batch chains
       # overlap); DEFER_LMHEAD peak memory
