@@ -174,11 +174,18 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 #ifndef GVL_ATTN_FWD_DIAG
 #define GVL_ATTN_FWD_DIAG 0
 #endif
-template <int G, bool DROP>
-__global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel(AttnP p) {
+#ifndef GVL_ATTN_ONE_BPC  // blocks per CU the one-tile forward is compiled for
+#define GVL_ATTN_ONE_BPC 6
+#endif
+// ONE (Tk <= 64: one key tile, G = 1): a single LDS stage (16 KiB) and a 6-blocks-per-CU register
+// budget, so the caption decoders' 1536 (b, h) blocks of T = 63 are one round of 256 CUs (4 blocks
+// per CU by registers and 5 by LDS made it 1.5 rounds).
+template <int G, bool DROP, bool ONE = false>
+__global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
+  static_assert(!ONE || G == 1, "one-tile forward: G = 1");
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = 64 * G;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][KT * D * 2];  // [stage][K,V]
+  __shared__ __attribute__((aligned(16))) char smem[ONE ? 1 : 2][2][KT * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   int64_t qt, h, b;
@@ -204,7 +211,8 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
     const int64_t lim = qblk0 + QT;
     if (lim < kend) kend = lim;
   }
-  const int nkt = (int)((kend + KT - 1) / KT);
+  const int nkt0 = (int)((kend + KT - 1) / KT);
+  const int nkt = ONE ? (nkt0 > 0 ? 1 : 0) : nkt0;
 
 #ifndef GVL_ATTN_FWD_V2
 #define GVL_ATTN_FWD_V2 1
@@ -237,13 +245,13 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
+    const bool more = !ONE && GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
     if (more) {
       load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
       load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
     }
-    const char* ks = smem[kt & 1][0];
-    const char* vs = smem[kt & 1][1];
+    const char* ks = smem[ONE ? 0 : (kt & 1)][0];
+    const char* vs = smem[ONE ? 0 : (kt & 1)][1];
     const int64_t k0 = (int64_t)kt * KT;
     float4_t sc[G][4];
 #pragma unroll
@@ -352,8 +360,8 @@ __global__ __launch_bounds__(NT, (G == 1 && !DROP) ? 4 : 2) void attn_fwd_kernel
 #endif
     }
     if (more) {
-      store_rows<false>(rk, smem[(kt + 1) & 1][0], tid);
-      store_rows<true>(rv, smem[(kt + 1) & 1][1], tid);
+      store_rows<false>(rk, smem[ONE ? 0 : ((kt + 1) & 1)][0], tid);
+      store_rows<true>(rv, smem[ONE ? 0 : ((kt + 1) & 1)][1], tid);
     }
 #if GVL_ATTN_FWD_DIAG == 3
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1389,6 +1397,16 @@ bool fwd_dma_enabled() {
   return on;
 }
 
+// One-tile forward (attn_fwd_kernel<1, *, true>) for Tk <= 64; GVL_ATTN_FWD_ONE=0: the two-stage
+// kernel (A/B).
+bool fwd_one_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_ATTN_FWD_ONE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Block count of the 1-D heavy-first grid (see tile_of_block); fill() bounds it.
 unsigned grid_1d(const gvl_attn_desc* d, int64_t ntile) { return (unsigned)(ntile * d->H * d->B); }
 
@@ -1406,6 +1424,9 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   } else if (G == 2) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
+  } else if (d->Tk <= KT && fwd_one_enabled()) {
+    if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true>, grid, dim3(NT), 0, s, p);
+    else gvl::launch_timed(attn_fwd_kernel<1, false, true>, grid, dim3(NT), 0, s, p);
   } else {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<1, false>, grid, dim3(NT), 0, s, p);

@@ -24,6 +24,21 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6n)  # one-tile short attention forward (attn_fwd_kernel<1, *, true>: single 16 KiB LDS stage, 63 / 72
+      # VGPRs, up to 8 blocks per CU): T = 63 decoder forward 1536 blocks in one round instead of 1.5.
+      # Bound: attn_fwd_kernel<1, *> is 3.9 % of the cross step, 2.8 % of the Q-Former step; a third
+      # off -> cross ~1.3 %, Q-Former ~0.9 %. A/B by GVL_ATTN_FWD_ONE=0.
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross or linear" tests/test_gpu_parity_bench.py
+  ktests full "qformer or cross or linear" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in 0 1; do
+    GVL_ATTN_FWD_ONE=$v timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_one${v}_$r.log 2>&1; fatal $? attn_$v
+    echo "== attn ONE=$v $r"; grep -v amdgpu.ids $O/attn_one${v}_$r.log | sed -n 2,5p
+  done; done
+  for r in 1 2; do for v in 0 1; do
+    GVL_ATTN_FWD_ONE=$v bench cross_o${v}_$r cross; GVL_ATTN_FWD_ONE=$v bench qf_o${v}_$r qformer
+  done; done
+  ;;
 r6m)  # attention address registers (tr_lane / frag_tr_imm: one VGPR per column block, the k-half
       # and row group as ds offsets; dK/dV slot offset opaque). Bound: ISA count per dK/dV query
       # tile 64 -> 12 v_add_u32 (of ~250 vector issues), forward / dQ key tile 29 -> 13; attention
