@@ -24,6 +24,20 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6o)  # split-K slabs of 256 x 192 tiles for the caption lm_head dX (M = 3968, N = 768, K = 50304: 64 x 4
+      # = 256 items, one full round, instead of 48 x 4 = 192 of 256 x 256). Bound: the launch is
+      # 4.4 % of the Q-Former step, 7.5 % of cross; a quarter off -> ~1.1 % / ~1.9 %.
+      # A/B by GVL_PP3_SPLIT192=0.
+  ktests kt "splitk or wgrad or gemm_lmhead or caption"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross or linear" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for v in 0 1; do
+    GVL_PP3_SPLIT192=$v timeout -k 10 120 python tools/gemm_one.py 3968 768 50304 0 1 3 -1 20 > $O/g_s${v}_$r.log 2>&1; fatal $? g_$v
+    echo "split192=$v $r $(grep -v amdgpu.ids $O/g_s${v}_$r.log | tail -1)"
+  done; done
+  for r in 1 2; do for v in 0 1; do
+    GVL_PP3_SPLIT192=$v bench cross_s${v}_$r cross; GVL_PP3_SPLIT192=$v bench qf_s${v}_$r qformer
+  done; done
+  ;;
 r6n)  # one-tile short attention forward (attn_fwd_kernel<1, *, true>: single 16 KiB LDS stage, 63 / 72
       # VGPRs, up to 8 blocks per CU): T = 63 decoder forward 1536 blocks in one round instead of 1.5.
       # Bound: attn_fwd_kernel<1, *> is 3.9 % of the cross step, 2.8 % of the Q-Former step; a third
