@@ -24,6 +24,22 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6p)  # T > 64 dQ kernel (G = 2, no dropout) compiled for 3 blocks per CU (168 VGPRs, 48 B of spill
+      # outside the unmasked loop) instead of 2 (192 VGPRs). Bound: dQ is 4.9 % of the LM step at
+      # 2 waves per SIMD with ~38 % of wave cycles waiting; a third more waves -> 10-15 % off dQ =
+      # 0.5-0.7 % of the LM step. A/B against libgvl_dq2.so (GVL_ATTN_DQ_BPC=2).
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "lm" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for v in dq2 new; do
+    L=$LIBDIR/libgvl.so; [ $v = dq2 ] && L=$LIBDIR/libgvl_dq2.so
+    GVL_LIB=$L timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_${v}_$r.log 2>&1; fatal $? attn_$v
+    echo "== attn $v $r"; grep -v amdgpu.ids $O/attn_${v}_$r.log | head -1
+  done; done
+  for r in 1 2; do for v in dq2 new; do
+    L=$LIBDIR/libgvl.so; [ $v = dq2 ] && L=$LIBDIR/libgvl_dq2.so
+    GVL_LIB=$L bench lm_${v}_$r lm
+  done; done
+  ;;
 r6o)  # split-K slabs of 256 x 192 tiles for the caption lm_head dX (M = 3968, N = 768, K = 50304: 64 x 4
       # = 256 items, one full round, instead of 48 x 4 = 192 of 256 x 256). Bound: the launch is
       # 4.4 % of the Q-Former step, 7.5 % of cross; a quarter off -> ~1.1 % / ~1.9 %.
