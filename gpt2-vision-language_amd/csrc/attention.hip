@@ -85,11 +85,11 @@ GVL_DEV void load_rows(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t r0
     else r[it] = make_uint4(0, 0, 0, 0);
   }
 }
-template <bool TR>
+template <bool TR, int NTH = NT>  // NTH threads store 2 * NTH / 8 rows
 GVL_DEV void store_rows(const uint4 (&r)[2], char* lds, int tid) {
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     const int off = TR ? swz_tr(row, ch) : swz_row(row, ch);
     *reinterpret_cast<uint4*>(lds + off) = r[it];
   }
@@ -121,10 +121,11 @@ GVL_DEV short8_t frag_tr(const char* lds, int t, int s, int lane) {
 // probability or score gradient, or not stored, so the results are unchanged; with no branch or
 // select on the loaded data hipcc issues the block's loads back to back and waits once, instead
 // of one round trip per conditional load (the prologue was six).
+template <int NTH = NT>
 GVL_DEV void load_rows_nb(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t R, int tid) {
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     r[it] = *reinterpret_cast<const uint4*>(base + (row < R ? row : 0) * st + ch * 8);
   }
 }
@@ -1132,7 +1133,7 @@ struct ShortIn {  // one (b, h)'s operands of the short backward, loaded ahead o
   uint4 rq[2], rk[2], rv[2], rd[2], oa[2];
   float lse_raw;
 };
-template <bool DROP>
+template <bool DROP, int R>
 GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn& in) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
@@ -1146,22 +1147,24 @@ GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn
   const int ql = wave * 16 + (lane & 15);
   const bool qok = ql < p.Tq;
   const int qlc = qok ? ql : 0;
-  load_rows_nb(in.rq, qbase, p.q_st, p.Tq, tid);
-  load_rows_nb(in.rk, kbase, p.k_st, p.Tk, tid);
-  load_rows_nb(in.rv, vbase, p.v_st, p.Tk, tid);
-  load_rows_nb(in.rd, dobase, gg.do_st, p.Tq, tid);
+  load_rows_nb<R * 4>(in.rq, qbase, p.q_st, p.Tq, tid);
+  load_rows_nb<R * 4>(in.rk, kbase, p.k_st, p.Tk, tid);
+  load_rows_nb<R * 4>(in.rv, vbase, p.v_st, p.Tk, tid);
+  load_rows_nb<R * 4>(in.rd, dobase, gg.do_st, p.Tq, tid);
 #pragma unroll
   for (int c = 0; c < 2; ++c) in.oa[c] = reinterpret_cast<const uint4*>(obase + qlc * p.o_st + 16 * Gl)[c];
   in.lse_raw = p.lse[bh * p.Tq + qlc];
 }
 
 // One (b, h) of the short backward from its loaded operands (bwd_short_load); smem: 4 (L32) or
-// 6 tiles of 64 x 64 bf16.
-template <bool DROP>
+// 6 tiles of R x 64 bf16.  R = 64: 4 waves (16 queries / keys each); R = 32 (Tq, Tk <= 32): 2
+// waves over 32-row tiles, one 32-deep k-step where R = 64 takes two.
+template <bool DROP, int R>
 GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const ShortIn& in,
                             char* smem0, uint64_t seed_) {
+  static_assert(R == 64 || R == 32, "short tile rows");
   constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
-  constexpr int TB = KT * D * 2;
+  constexpr int TB = R * D * 2, NG = R / 16, NKS = R / 32;  // key groups of 16, 32-deep k-steps
   char* const qs = smem0;
   char* const ks = smem0 + TB;
   char* const vs = smem0 + 2 * TB;
@@ -1181,7 +1184,7 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     uint32_t x = in.oa[0].x ^ in.oa[1].y ^ __float_as_uint(lse_raw);
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+      const int row = (tid >> 3) + (R / 2) * it, ch = tid & 7;
       if (row < p.Tq) {
         *reinterpret_cast<uint4*>(gg.dq + b * gg.dq_sb + h * gg.dq_sh + row * gg.dq_st + ch * 8) = rq[it] ^ make_uint4(x, x, x, x);
         *reinterpret_cast<uint4*>(gg.dk + b * gg.dk_sb + h * gg.dk_sh + row * gg.dk_st + ch * 8) = rk[it] ^ rd[it];
@@ -1190,10 +1193,10 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     }
     return;
   }
-  store_rows<false>(rq, qs, tid);
-  store_rows<false>(rk, ks, tid);
-  store_rows<false>(rv, vs, tid);
-  store_rows<false>(rd, ds, tid);
+  store_rows<false, R * 4>(rq, qs, tid);
+  store_rows<false, R * 4>(rk, ks, tid);
+  store_rows<false, R * 4>(rv, vs, tid);
+  store_rows<false, R * 4>(rd, ds, tid);
   __syncthreads();
   // this lane's Q / dO fragments and dO row piece from the LDS tiles (rows past Tq hold row 0,
   // as load_rows_nb staged them: the data the global fragment loads used to fetch)
@@ -1218,9 +1221,9 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
   if (!qok) Dq = 0.f;
   const float lse2 = qok ? lse_raw * LOG2E : 0.f;
   Dq = swap32_reduce<false>(swap16_reduce<false>(Dq));  // the row's 4 lanes (VALU swaps)
-  float4_t sc[4], dp[4];
+  float4_t sc[NG], dp[NG];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
+  for (int n = 0; n < NG; ++n) {
     sc[n] = float4_t{0.f, 0.f, 0.f, 0.f};
     dp[n] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1230,9 +1233,9 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     }
   }
   const uint64_t drow0 = (uint64_t)ridx * (uint64_t)p.Tk;
-  float4_t pd[4];
+  float4_t pd[NG];
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NG; ++n)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int kk = 16 * n + 4 * Gl + r;
@@ -1248,15 +1251,15 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
       sc[n][r] = pv * (dpv - Dq);  // dS
     }
   // P and dS to LDS as [query][key]: lane (query ql) owns keys 16n + 4Gl .. +3 (8 bytes)
-  uint2 pw[4], sw[4];
+  uint2 pw[NG], sw[NG];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
+  for (int n = 0; n < NG; ++n) {
     pw[n] = make_uint2(pack2(pd[n][0], pd[n][1]), pack2(pd[n][2], pd[n][3]));
     sw[n] = make_uint2(pack2(sc[n][0], sc[n][1]), pack2(sc[n][2], sc[n][3]));
   }
   auto store_p_ds = [&]() {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NG; ++n) {
       const int off = swz_tr(ql, 2 * n + (Gl >> 1)) + (Gl & 1) * 8;
       *reinterpret_cast<uint2*>(ps + off) = pw[n];
       *reinterpret_cast<uint2*>(ss + off) = sw[n];
@@ -1264,12 +1267,13 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
   };
   if constexpr (!L32) store_p_ds();
   {  // dQ = dS K (lane-local dS fragments, K read transposed)
-    const short8_t sf0 = pack_frag(sc[0], sc[1]), sf1 = pack_frag(sc[2], sc[3]);
+    const short8_t sf0 = pack_frag(sc[0], sc[1]);
+    const short8_t sf1 = NKS == 2 ? pack_frag(sc[NG - 2], sc[NG - 1]) : sf0;
     float4_t acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       acc[t] = mfma16(frag_tr<false>(ks, t, 0, lane), sf0, float4_t{0.f, 0.f, 0.f, 0.f});
-      acc[t] = mfma16(frag_tr<false>(ks, t, 1, lane), sf1, acc[t]);
+      if constexpr (NKS == 2) acc[t] = mfma16(frag_tr<false>(ks, t, 1, lane), sf1, acc[t]);
     }
     if (qok) {
       bf16_t* dst = gg.dq + b * gg.dq_sb + h * gg.dq_sh + ql * gg.dq_st;
@@ -1294,7 +1298,7 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+  for (int s2 = 0; s2 < NKS; ++s2) {
     const short8_t pf = frag_tr<false>(ps, wave, s2, lane);
     const short8_t sf = frag_tr<false>(ss, wave, s2, lane);
 #pragma unroll
@@ -1322,14 +1326,17 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
 // math, at 3 waves per SIMD: no faster — T = 63 0.023-0.024 vs 0.023 ms, T = 32 with dropout
 // 0.020 vs 0.018 ms; Q-Former / cross / linear steps 0.1-0.9 % slower; profiles/r6/
 // attn_short_pair_r6d.txt — and was removed.)
-template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
+// R = 32 (Tq, Tk <= 32: the cross-att decoder's 31-token self-attention, the Q-Former bridge's
+// 32 queries): 2 waves and 16 KiB of LDS per (b, h) instead of 4 waves over 64-row tiles half of
+// whose rows and waves were padding (5 blocks per CU by LDS -> 10).
+template <bool DROP, int R = 64>
+__global__ __launch_bounds__(R * 4, R == 64 ? 2 : 5) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
-  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][KT * D * 2];
+  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][R * D * 2];
   ShortIn in;
-  bwd_short_load<DROP>(p, gg, blockIdx.x, in);
-  bwd_short_item<DROP>(p, gg, blockIdx.x, in, smem[0], seed_);
+  bwd_short_load<DROP, R>(p, gg, blockIdx.x, in);
+  bwd_short_item<DROP, R>(p, gg, blockIdx.x, in, smem[0], seed_);
 }
 
 int fill(const gvl_attn_desc* d, AttnP& p) {
@@ -1392,6 +1399,16 @@ bool short_bwd_enabled() {
 bool fwd_dma_enabled() {
   static const bool on = [] {
     const char* e = getenv("GVL_ATTN_FWD_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// 32-row short backward (attn_bwd_short_kernel<*, 32>) for Tq, Tk <= 32; GVL_ATTN_SHORT32=0: the
+// 64-row kernel (A/B).
+bool short32_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_ATTN_SHORT32");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1462,8 +1479,13 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
   hipStream_t s = gvl::as_stream(stream);
   if (d->Tq <= 64 && d->Tk <= 64 && short_bwd_enabled()) {
     dim3 grid((unsigned)(d->B * d->H));
-    if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true>, grid, dim3(NT), 0, s, p, g);
-    else gvl::launch_timed(attn_bwd_short_kernel<false>, grid, dim3(NT), 0, s, p, g);
+    if (d->Tq <= 32 && d->Tk <= 32 && short32_enabled()) {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true, 32>, grid, dim3(128), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_short_kernel<false, 32>, grid, dim3(128), 0, s, p, g);
+    } else {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true>, grid, dim3(NT), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_short_kernel<false>, grid, dim3(NT), 0, s, p, g);
+    }
     GVL_LAUNCH_CHECK("gvl_attn_bwd(short)");
     return 0;
   }

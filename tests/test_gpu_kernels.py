@@ -1082,17 +1082,18 @@ def _attn_case(cuda, B, H, Tq, Tk, causal, packed, drop_p=0.0, seed=0, grad=True
 
 
 @pytest.mark.parametrize("B,H,T", [(2, 2, 80), (1, 2, 1024), (2, 2, 300), (3, 12, 63), (2, 3, 64), (1, 1, 7),
-                                   (3, 3, 50), (40, 12, 31)])
+                                   (3, 3, 50), (40, 12, 31), (5, 12, 32), (2, 2, 1), (2, 3, 17)])
 def test_attention_causal(cuda, B, H, T):
     _attn_case(cuda, B, H, T, T, True, packed=True)
 
 
-@pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257), (40, 130), (130, 1000)])
+@pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257), (40, 130), (130, 1000),
+                                   (1, 32), (20, 9)])
 def test_attention_noncausal(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False)
 
 
-@pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130)])
+@pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130), (32, 32), (17, 29)])
 def test_attention_dropout_exact_mask(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False, drop_p=0.1, seed=4242)
 
@@ -1100,12 +1101,15 @@ def test_attention_dropout_exact_mask(cuda, Tq, Tk):
 def test_attention_short_over_nan_filled_memory(cuda):
     """The single-launch short backward (Q / dO fragments and the dO row piece of D read back
     from its LDS tiles) repeated over NaN-filled free memory, causal 63-token and dropout 32 x 33
-    cases: any byte read before it is written shows up as an intermittent error."""
+    cases, and the 32-row kernel's causal 31-token and dropout 32 x 32 cases: any byte read before
+    it is written shows up as an intermittent error."""
     for it in range(6):
         junk = torch.full((32 << 20,), float("nan"), device=cuda)
         del junk
         _attn_case(cuda, 4, 6, 63, 63, True, packed=True)
         _attn_case(cuda, 3, 2, 32, 33, False, packed=False, drop_p=0.1, seed=77 + it)
+        _attn_case(cuda, 4, 6, 31, 31, True, packed=True)
+        _attn_case(cuda, 3, 2, 32, 32, False, packed=False, drop_p=0.1, seed=91 + it)
 
 
 def test_attention_bwd_repeats_over_nan_filled_memory(cuda):

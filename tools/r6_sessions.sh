@@ -24,6 +24,34 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6q2)  # r6q's A/B was within noise at the step level: kernel durations by rocprofv3 (attn_one 50
+       # iterations each) and three more alternated cross / Q-Former pairs
+  for v in 0 1; do
+    GVL_ATTN_SHORT32=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s$v -o s$v -- \
+      python tools/attn_one.py 50 > $O/prof_s$v.log 2>&1; fatal $? prof_s$v
+    f=$(find $O/prof_s$v -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 12 > $O/table_s$v.txt
+    echo "== SHORT32=$v"; grep -E "short|attn_fwd_kernel" $O/table_s$v.txt
+  done
+  for r in 1 2 3; do for v in 0 1; do
+    GVL_ATTN_SHORT32=$v bench cross_s${v}_$r cross; GVL_ATTN_SHORT32=$v bench qf_s${v}_$r qformer
+  done; done
+  ;;
+r6q)  # 32-row short attention backward (attn_bwd_short_kernel<*, 32>: 2 waves, 16 KiB LDS, 56 VGPRs) for
+      # Tq, Tk <= 32: the cross-att decoder's 31-token self-attention (12 per step) and the Q-Former
+      # bridge's 32-query self-attention. Bound: attn_bwd_short is 6.2 % of the cross step, half of it
+      # T = 31; 64-row blocks were half padding at 5 per CU -> ~40 % off those = ~1.2 % of cross,
+      # ~0.4 % of the Q-Former step. A/B by GVL_ATTN_SHORT32=0.
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross" tests/test_gpu_parity_bench.py
+  ktests full "qformer or cross" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in 0 1; do
+    GVL_ATTN_SHORT32=$v timeout -k 10 200 python -u tools/attn_one.py 30 > $O/attn_s${v}_$r.log 2>&1; fatal $? attn_$v
+    echo "== attn SHORT32=$v $r"; grep -v amdgpu.ids $O/attn_s${v}_$r.log | sed -n 3,4p
+  done; done
+  for r in 1 2; do for v in 0 1; do
+    GVL_ATTN_SHORT32=$v bench cross_s${v}_$r cross; GVL_ATTN_SHORT32=$v bench qf_s${v}_$r qformer
+  done; done
+  ;;
 r6p)  # T > 64 dQ kernel (G = 2, no dropout) compiled for 3 blocks per CU (168 VGPRs, 48 B of spill
       # outside the unmasked loop) instead of 2 (192 VGPRs). Bound: dQ is 4.9 % of the LM step at
       # 2 waves per SIMD with ~38 % of wave cycles waiting; a third more waves -> 10-15 % off dQ =
