@@ -76,11 +76,12 @@ GVL_DEV void tile_of_block(const AttnP& p, int64_t ntile, int64_t& t, int64_t& h
 GVL_DEV int swz_tr(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
 GVL_DEV int swz_row(int row, int chunk) { return swz_tr(row, chunk); }
 
-// Register-stage a 64x64 tile (rows r0.., valid rows < R) from a strided tensor.
+// Register-stage a (2 * NTH / 8) x 64 tile (rows r0.., valid rows < R) from a strided tensor.
+template <int NTH = NT>
 GVL_DEV void load_rows(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t r0, int64_t R, int tid) {
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int row = (tid >> 3) + 32 * it, ch = tid & 7;
+    const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     if (r0 + row < R) r[it] = *reinterpret_cast<const uint4*>(base + (r0 + row) * st + ch * 8);
     else r[it] = make_uint4(0, 0, 0, 0);
   }
@@ -181,12 +182,17 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 // ONE (Tk <= 64: one key tile, G = 1): a single LDS stage (16 KiB) and a 6-blocks-per-CU register
 // budget, so the caption decoders' 1536 (b, h) blocks of T = 63 are one round of 256 CUs (4 blocks
 // per CU by registers and 5 by LDS made it 1.5 rounds).
-template <int G, bool DROP, bool ONE = false>
-__global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
+// R = 32 (ONE, Tq, Tk <= 32: the cross-att decoder's 31-token self-attention, the Q-Former
+// bridge's 32 queries): 2 waves over 32-row Q / K / V tiles instead of 4 waves over 64-row ones
+// half of which were padding.
+template <int G, bool DROP, bool ONE = false, int R = 64>
+__global__ __launch_bounds__(R * 4, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
   static_assert(!ONE || G == 1, "one-tile forward: G = 1");
+  static_assert(R == 64 || (R == 32 && ONE), "32-row tiles: one-tile forward only");
+  constexpr int NG = R / 16, NKS = R / 32;  // key groups of 16, 32-deep k-steps per key tile
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
-  constexpr int QT = 64 * G;
-  __shared__ __attribute__((aligned(16))) char smem[ONE ? 1 : 2][2][KT * D * 2];  // [stage][K,V]
+  constexpr int QT = R == 32 ? 32 : 64 * G;
+  __shared__ __attribute__((aligned(16))) char smem[ONE ? 1 : 2][2][R * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   int64_t qt, h, b;
@@ -239,24 +245,24 @@ __global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
 
   uint4 rk[2], rv[2];
-  load_rows(rk, kbase, p.k_st, 0, p.Tk, tid);
-  load_rows(rv, vbase, p.v_st, 0, p.Tk, tid);
-  store_rows<false>(rk, smem[0][0], tid);
-  store_rows<true>(rv, smem[0][1], tid);
+  load_rows<R * 4>(rk, kbase, p.k_st, 0, p.Tk, tid);
+  load_rows<R * 4>(rv, vbase, p.v_st, 0, p.Tk, tid);
+  store_rows<false, R * 4>(rk, smem[0][0], tid);
+  store_rows<true, R * 4>(rv, smem[0][1], tid);
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
     const bool more = !ONE && GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
     if (more) {
-      load_rows(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
-      load_rows(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows<R * 4>(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows<R * 4>(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
     }
     const char* ks = smem[ONE ? 0 : (kt & 1)][0];
     const char* vs = smem[ONE ? 0 : (kt & 1)][1];
     const int64_t k0 = (int64_t)kt * KT;
-    float4_t sc[G][4];
+    float4_t sc[G][NG];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NG; ++n) {
 #pragma unroll
       for (int g = 0; g < G; ++g) sc[g][n] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -272,10 +278,10 @@ __global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4
       // lane holds raw S[q][key = k0 + 16n + 4Gl + r]; masks only on boundary / diagonal
       // tiles (wave-uniform test), the softmax scale folded into the exp2 argument
       const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
-      if (k0 + KT > p.Tk || (p.causal && k0 + KT - 1 > qg0)) {
+      if (k0 + R > p.Tk || (p.causal && k0 + R - 1 > qg0)) {
         const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < NG; ++n)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int kk = 16 * n + 4 * Gl + r;
@@ -285,11 +291,13 @@ __global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4
       float mx = fmaxf(fmaxf(sc[g][0][0], sc[g][0][1]), sc[g][0][2]);
       mx = fmaxf(fmaxf(mx, sc[g][0][3]), sc[g][1][0]);
       mx = fmaxf(fmaxf(mx, sc[g][1][1]), sc[g][1][2]);
-      mx = fmaxf(fmaxf(mx, sc[g][1][3]), sc[g][2][0]);
-      mx = fmaxf(fmaxf(mx, sc[g][2][1]), sc[g][2][2]);
-      mx = fmaxf(fmaxf(mx, sc[g][2][3]), sc[g][3][0]);
-      mx = fmaxf(fmaxf(mx, sc[g][3][1]), sc[g][3][2]);
-      mx = fmaxf(mx, sc[g][3][3]);
+      mx = fmaxf(mx, sc[g][1][3]);
+      if constexpr (NG == 4) {
+        mx = fmaxf(fmaxf(mx, sc[g][NG - 2][0]), sc[g][NG - 2][1]);
+        mx = fmaxf(fmaxf(mx, sc[g][NG - 2][2]), sc[g][NG - 2][3]);
+        mx = fmaxf(fmaxf(mx, sc[g][NG - 1][0]), sc[g][NG - 1][1]);
+        mx = fmaxf(fmaxf(mx, sc[g][NG - 1][2]), sc[g][NG - 1][3]);
+      }
       mx = rowmax4(mx);
 #if GVL_ATTN_FWD_V2
       // deferred rescale (T13): keep the running max while no row's max grew by more than
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4
 #endif
       const uint64_t drow = (((uint64_t)b * p.H + h) * p.Tq + (uint64_t)q[g]) * (uint64_t)p.Tk;
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < NG; ++n)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
 #if GVL_ATTN_FWD_DIAG == 1
@@ -340,13 +348,13 @@ __global__ __launch_bounds__(NT, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4
       for (int t = 0; t < 4; ++t) o[g][t] *= alpha;
 #endif
       pf[g][0] = pack_frag(sc[g][0], sc[g][1]);
-      pf[g][1] = pack_frag(sc[g][2], sc[g][3]);
+      if constexpr (NKS == 2) pf[g][1] = pack_frag(sc[g][NG - 2], sc[g][NG - 1]);
 #if GVL_ATTN_FWD_V2
       if constexpr (DROP) l[g] += ls;
 #endif
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NKS; ++s) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const short8_t vf = frag_tr<true>(vs, t, s, lane);
@@ -1441,6 +1449,10 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
   } else if (G == 2) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<2, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<2, false>, grid, dim3(NT), 0, s, p);
+  } else if (d->Tq <= 32 && d->Tk <= 32 && fwd_one_enabled() && short32_enabled()) {
+    dim3 g32(grid_1d(d, 1));
+    if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true, 32>, g32, dim3(128), 0, s, p);
+    else gvl::launch_timed(attn_fwd_kernel<1, false, true, 32>, g32, dim3(128), 0, s, p);
   } else if (d->Tk <= KT && fwd_one_enabled()) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<1, false, true>, grid, dim3(NT), 0, s, p);

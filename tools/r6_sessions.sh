@@ -24,6 +24,22 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6r)  # 32-row one-tile forward (attn_fwd_kernel<1, *, true, 32>: 2 waves, 8 KiB LDS) with the r6q backward
+      # under the same switch (GVL_ATTN_SHORT32). Bound: the T = 31 forward is ~9 us x 12 per cross step
+      # with half its waves idle -> ~3 us each = ~0.6 % of cross. Kernel stats (rocprofv3) + steps.
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross" tests/test_gpu_parity_bench.py
+  ktests full "qformer or cross" tests/test_gpu_parity_full.py
+  for v in 0 1; do
+    GVL_ATTN_SHORT32=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s$v -o s$v -- \
+      python tools/attn_one.py 50 > $O/prof_s$v.log 2>&1; fatal $? prof_s$v
+    f=$(find $O/prof_s$v -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 12 > $O/table_s$v.txt
+    echo "== SHORT32=$v"; grep -E "short|attn_fwd_kernel" $O/table_s$v.txt
+  done
+  for r in 1 2 3; do for v in 0 1; do
+    GVL_ATTN_SHORT32=$v bench cross_s${v}_$r cross; GVL_ATTN_SHORT32=$v bench qf_s${v}_$r qformer
+  done; done
+  ;;
 r6q2)  # r6q's A/B was within noise at the step level: kernel durations by rocprofv3 (attn_one 50
        # iterations each) and three more alternated cross / Q-Former pairs
   for v in 0 1; do
