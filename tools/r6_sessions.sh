@@ -24,6 +24,24 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6s)  # 16 KiB short attention backward (attn_bwd_short16_kernel: never more than two 64-row tiles in LDS,
+      # 76 VGPRs) for 32 < T <= 64: 6 blocks per CU instead of 5, the 1536 (b, h) blocks of the
+      # Q-Former / linear decoders in one round. Bound: attn_bwd_short<false, 64> is 3.4 % of the
+      # Q-Former step (22.3 us x 12); 1.2 rounds -> 1 at ~equal block time -> up to ~15 % off = ~0.5 %.
+      # A/B by GVL_ATTN_SHORT16=0 (kernel stats + steps).
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or linear or cross" tests/test_gpu_parity_bench.py
+  ktests full "qformer or linear or cross" tests/test_gpu_parity_full.py
+  for v in 0 1; do
+    GVL_ATTN_SHORT16=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s$v -o s$v -- \
+      python tools/attn_one.py 50 > $O/prof_s$v.log 2>&1; fatal $? prof_s$v
+    f=$(find $O/prof_s$v -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 12 > $O/table_s$v.txt
+    echo "== SHORT16=$v"; grep -E "short" $O/table_s$v.txt
+  done
+  for r in 1 2 3; do for v in 0 1; do
+    GVL_ATTN_SHORT16=$v bench qf_s${v}_$r qformer; GVL_ATTN_SHORT16=$v bench lin_s${v}_$r linear
+  done; done
+  ;;
 r6r)  # 32-row one-tile forward (attn_fwd_kernel<1, *, true, 32>: 2 waves, 8 KiB LDS) with the r6q backward
       # under the same switch (GVL_ATTN_SHORT32). Bound: the T = 31 forward is ~9 us x 12 per cross step
       # with half its waves idle -> ~3 us each = ~0.6 % of cross. Kernel stats (rocprofv3) + steps.
