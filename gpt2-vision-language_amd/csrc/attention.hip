@@ -77,19 +77,19 @@ GVL_DEV int swz_tr(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 
 GVL_DEV int swz_row(int row, int chunk) { return swz_tr(row, chunk); }
 
 // Register-stage a (2 * NTH / 8) x 64 tile (rows r0.., valid rows < R) from a strided tensor.
-template <int NTH = NT>
-GVL_DEV void load_rows(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t r0, int64_t R, int tid) {
+template <int NTH = NT, int NC = 2>  // NTH threads, NC 16-B chunks each: NC * NTH / 8 rows
+GVL_DEV void load_rows(uint4 (&r)[NC], const bf16_t* base, int64_t st, int64_t r0, int64_t R, int tid) {
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < NC; ++it) {
     const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     if (r0 + row < R) r[it] = *reinterpret_cast<const uint4*>(base + (r0 + row) * st + ch * 8);
     else r[it] = make_uint4(0, 0, 0, 0);
   }
 }
-template <bool TR, int NTH = NT>  // NTH threads store 2 * NTH / 8 rows
-GVL_DEV void store_rows(const uint4 (&r)[2], char* lds, int tid) {
+template <bool TR, int NTH = NT, int NC = 2>  // NTH threads store NC * NTH / 8 rows
+GVL_DEV void store_rows(const uint4 (&r)[NC], char* lds, int tid) {
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < NC; ++it) {
     const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     const int off = TR ? swz_tr(row, ch) : swz_row(row, ch);
     *reinterpret_cast<uint4*>(lds + off) = r[it];
@@ -122,10 +122,10 @@ GVL_DEV short8_t frag_tr(const char* lds, int t, int s, int lane) {
 // probability or score gradient, or not stored, so the results are unchanged; with no branch or
 // select on the loaded data hipcc issues the block's loads back to back and waits once, instead
 // of one round trip per conditional load (the prologue was six).
-template <int NTH = NT>
-GVL_DEV void load_rows_nb(uint4 (&r)[2], const bf16_t* base, int64_t st, int64_t R, int tid) {
+template <int NTH = NT, int NC = 2>
+GVL_DEV void load_rows_nb(uint4 (&r)[NC], const bf16_t* base, int64_t st, int64_t R, int tid) {
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < NC; ++it) {
     const int row = (tid >> 3) + (NTH / 8) * it, ch = tid & 7;
     r[it] = *reinterpret_cast<const uint4*>(base + (row < R ? row : 0) * st + ch * 8);
   }
@@ -185,14 +185,15 @@ GVL_DEV short8_t pack_frag(const float4_t& a, const float4_t& b) {
 // R = 32 (ONE, Tq, Tk <= 32: the cross-att decoder's 31-token self-attention, the Q-Former
 // bridge's 32 queries): 2 waves over 32-row Q / K / V tiles instead of 4 waves over 64-row ones
 // half of which were padding.
-template <int G, bool DROP, bool ONE = false, int R = 64>
-__global__ __launch_bounds__(R * 4, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
+template <int G, bool DROP, bool ONE = false, int R = 64, int RK = R>  // R: query rows, RK: key rows
+__global__ __launch_bounds__(R * 4, ONE ? (RK > R ? 5 : GVL_ATTN_ONE_BPC) : ((G == 1 && !DROP) ? 4 : 2)) void attn_fwd_kernel(AttnP p) {
   static_assert(!ONE || G == 1, "one-tile forward: G = 1");
-  static_assert(R == 64 || (R == 32 && ONE), "32-row tiles: one-tile forward only");
-  constexpr int NG = R / 16, NKS = R / 32;  // key groups of 16, 32-deep k-steps per key tile
+  static_assert((R == 64 && RK == 64) || (R == 32 && ONE && (RK == 32 || RK == 64)), "tile rows");
+  constexpr int NG = RK / 16, NKS = RK / 32;  // key groups of 16, 32-deep k-steps per key tile
+  constexpr int NC = 2 * RK / R;             // 16-B chunks per thread of a K / V tile
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr int QT = R == 32 ? 32 : 64 * G;
-  __shared__ __attribute__((aligned(16))) char smem[ONE ? 1 : 2][2][R * D * 2];  // [stage][K,V]
+  __shared__ __attribute__((aligned(16))) char smem[ONE ? 1 : 2][2][RK * D * 2];  // [stage][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   int64_t qt, h, b;
@@ -244,18 +245,18 @@ __global__ __launch_bounds__(R * 4, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) 
 #pragma unroll
   for (int k = 0; k < 8; ++k) ones[k] = (short)0x3F80;  // bf16 1.0
 
-  uint4 rk[2], rv[2];
-  load_rows<R * 4>(rk, kbase, p.k_st, 0, p.Tk, tid);
-  load_rows<R * 4>(rv, vbase, p.v_st, 0, p.Tk, tid);
-  store_rows<false, R * 4>(rk, smem[0][0], tid);
-  store_rows<true, R * 4>(rv, smem[0][1], tid);
+  uint4 rk[NC], rv[NC];
+  load_rows<R * 4, NC>(rk, kbase, p.k_st, 0, p.Tk, tid);
+  load_rows<R * 4, NC>(rv, vbase, p.v_st, 0, p.Tk, tid);
+  store_rows<false, R * 4, NC>(rk, smem[0][0], tid);
+  store_rows<true, R * 4, NC>(rv, smem[0][1], tid);
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
     const bool more = !ONE && GVL_ATTN_FWD_DIAG != 2 && kt + 1 < nkt;
     if (more) {
-      load_rows<R * 4>(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
-      load_rows<R * 4>(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows<R * 4, NC>(rk, kbase, p.k_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
+      load_rows<R * 4, NC>(rv, vbase, p.v_st, (int64_t)(kt + 1) * KT, p.Tk, tid);
     }
     const char* ks = smem[ONE ? 0 : (kt & 1)][0];
     const char* vs = smem[ONE ? 0 : (kt & 1)][1];
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(R * 4, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) 
       // lane holds raw S[q][key = k0 + 16n + 4Gl + r]; masks only on boundary / diagonal
       // tiles (wave-uniform test), the softmax scale folded into the exp2 argument
       const int64_t qg0 = qblk0 + wave * 16 * G + g * 16;
-      if (k0 + R > p.Tk || (p.causal && k0 + R - 1 > qg0)) {
+      if (k0 + RK > p.Tk || (p.causal && k0 + RK - 1 > qg0)) {
         const int kl = (int)(p.Tk - k0), ql = (int)(q[g] - k0);
 #pragma unroll
         for (int n = 0; n < NG; ++n)
@@ -369,8 +370,8 @@ __global__ __launch_bounds__(R * 4, ONE ? GVL_ATTN_ONE_BPC : ((G == 1 && !DROP) 
 #endif
     }
     if (more) {
-      store_rows<false>(rk, smem[ONE ? 0 : ((kt + 1) & 1)][0], tid);
-      store_rows<true>(rv, smem[ONE ? 0 : ((kt + 1) & 1)][1], tid);
+      store_rows<false, R * 4, NC>(rk, smem[ONE ? 0 : ((kt + 1) & 1)][0], tid);
+      store_rows<true, R * 4, NC>(rv, smem[ONE ? 0 : ((kt + 1) & 1)][1], tid);
     }
 #if GVL_ATTN_FWD_DIAG == 3
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1137,12 +1138,14 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(AttnP p) {
 #ifndef GVL_ATTN_SHORT_DIAG
 #define GVL_ATTN_SHORT_DIAG 0
 #endif
+template <int NCK>
 struct ShortIn {  // one (b, h)'s operands of the short backward, loaded ahead of its math
-  uint4 rq[2], rk[2], rv[2], rd[2], oa[2];
+  uint4 rq[2], rk[NCK], rv[NCK], rd[2], oa[2];
   float lse_raw;
 };
-template <bool DROP, int R>
-GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn& in) {
+template <bool DROP, int R, int RK>
+GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn<2 * RK / R>& in) {
+  constexpr int NCK = 2 * RK / R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   const int64_t b = bh / p.H, h = bh - b * p.H;
@@ -1156,39 +1159,44 @@ GVL_DEV void bwd_short_load(const AttnP& p, const AttnG& gg, int64_t bh, ShortIn
   const bool qok = ql < p.Tq;
   const int qlc = qok ? ql : 0;
   load_rows_nb<R * 4>(in.rq, qbase, p.q_st, p.Tq, tid);
-  load_rows_nb<R * 4>(in.rk, kbase, p.k_st, p.Tk, tid);
-  load_rows_nb<R * 4>(in.rv, vbase, p.v_st, p.Tk, tid);
+  load_rows_nb<R * 4, NCK>(in.rk, kbase, p.k_st, p.Tk, tid);
+  load_rows_nb<R * 4, NCK>(in.rv, vbase, p.v_st, p.Tk, tid);
   load_rows_nb<R * 4>(in.rd, dobase, gg.do_st, p.Tq, tid);
 #pragma unroll
   for (int c = 0; c < 2; ++c) in.oa[c] = reinterpret_cast<const uint4*>(obase + qlc * p.o_st + 16 * Gl)[c];
   in.lse_raw = p.lse[bh * p.Tq + qlc];
 }
 
-// One (b, h) of the short backward from its loaded operands (bwd_short_load); smem: 4 (L32) or
-// 6 tiles of R x 64 bf16.  R = 64: 4 waves (16 queries / keys each); R = 32 (Tq, Tk <= 32): 2
-// waves over 32-row tiles, one 32-deep k-step where R = 64 takes two.
-template <bool DROP, int R>
-GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const ShortIn& in,
+// One (b, h) of the short backward from its loaded operands (bwd_short_load); smem: the Q / dO
+// tiles of R rows, the K / V tiles of RK rows, and P / dS ([query][key], R rows) over V / K (L32)
+// or after them.  R = RK = 64: 4 waves (16 queries / keys each); R = 32 (Tq <= 32): 2 waves over
+// 32-row query tiles, each wave taking RK / 32 key groups of 16 in phase 2; RK = 32 (Tk <= 32):
+// one 32-deep k-step over the keys where 64 take two.
+template <bool DROP, int R, int RK>
+GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const ShortIn<2 * RK / R>& in,
                             char* smem0, uint64_t seed_) {
-  static_assert(R == 64 || R == 32, "short tile rows");
+  static_assert((R == 64 && RK == 64) || (R == 32 && (RK == 32 || RK == 64)), "short tile rows");
   constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
-  constexpr int TB = R * D * 2, NG = R / 16, NKS = R / 32;  // key groups of 16, 32-deep k-steps
+  constexpr int TQ = R * D * 2, TK = RK * D * 2;
+  constexpr int NG = RK / 16, NKS = RK / 32;  // key groups of 16, 32-deep k-steps over the keys
+  constexpr int NQS = R / 32, KPW = RK / R;   // k-steps over the queries; key groups per wave
+  constexpr int NCK = 2 * RK / R;
   char* const qs = smem0;
-  char* const ks = smem0 + TB;
-  char* const vs = smem0 + 2 * TB;
-  char* const ds = smem0 + 3 * TB;
-  char* const ps = smem0 + (L32 ? 2 : 4) * TB;  // (L32: over V)
-  char* const ss = smem0 + (L32 ? 1 : 5) * TB;  // (L32: over K)
+  char* const ks = smem0 + TQ;
+  char* const vs = smem0 + TQ + TK;
+  char* const ds = smem0 + TQ + 2 * TK;
+  char* const ps = L32 ? vs : smem0 + 2 * TQ + 2 * TK;       // (L32: over V)
+  char* const ss = L32 ? ks : smem0 + 3 * TQ + 2 * TK;       // (L32: over K)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Gl = lane >> 4;
   const int64_t b = bh / p.H, h = bh - b * p.H;
   const int ql = wave * 16 + (lane & 15);
   const bool qok = ql < p.Tq;
   const int64_t ridx = bh * p.Tq + ql;
-  const uint4 (&rq)[2] = in.rq, (&rk)[2] = in.rk, (&rv)[2] = in.rv, (&rd)[2] = in.rd;
+  const uint4 (&rq)[2] = in.rq, (&rk)[NCK] = in.rk, (&rv)[NCK] = in.rv, (&rd)[2] = in.rd;
   const uint4 (&oa)[2] = in.oa;
   const float lse_raw = in.lse_raw;
-  if constexpr (GVL_ATTN_SHORT_DIAG == 1) {  // timing-only: the loads, then stores of the same bytes
+  if constexpr (GVL_ATTN_SHORT_DIAG == 1 && R == RK) {  // timing-only: the loads, then stores of the same bytes
     uint32_t x = in.oa[0].x ^ in.oa[1].y ^ __float_as_uint(lse_raw);
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
@@ -1202,8 +1210,8 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     return;
   }
   store_rows<false, R * 4>(rq, qs, tid);
-  store_rows<false, R * 4>(rk, ks, tid);
-  store_rows<false, R * 4>(rv, vs, tid);
+  store_rows<false, R * 4, NCK>(rk, ks, tid);
+  store_rows<false, R * 4, NCK>(rv, vs, tid);
   store_rows<false, R * 4>(rd, ds, tid);
   __syncthreads();
   // this lane's Q / dO fragments and dO row piece from the LDS tiles (rows past Tq hold row 0,
@@ -1297,35 +1305,39 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
     store_p_ds();
   }
   __syncthreads();
-  // phase 2: this lane's key; P^T / dS^T fragments in the dK/dV kernel's k-slot order
-  const int kl = wave * 16 + (lane & 15);
-  float4_t dk[4], dv[4];
+  // phase 2: this lane's key (key groups wave, wave + R / 16 when RK > R); P^T / dS^T fragments
+  // in the dK/dV kernel's k-slot order
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-    dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < NKS; ++s2) {
-    const short8_t pf = frag_tr<false>(ps, wave, s2, lane);
-    const short8_t sf = frag_tr<false>(ss, wave, s2, lane);
+  for (int j = 0; j < KPW; ++j) {
+    const int kg = wave + (R / 16) * j, kl = kg * 16 + (lane & 15);
+    float4_t dk[4], dv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      dv[t] = mfma16(frag_tr<false>(ds, t, s2, lane), pf, dv[t]);
-      dk[t] = mfma16(frag_tr<false>(qs, t, s2, lane), sf, dk[t]);
+      dk[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+      dv[t] = float4_t{0.f, 0.f, 0.f, 0.f};
     }
-  }
-  if (kl < p.Tk) {
-    bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + kl * gg.dk_st;
-    bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + kl * gg.dv_st;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int d = 16 * t + 4 * Gl;
-      *reinterpret_cast<uint2*>(dkr + d) =
-          make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale),
-                     pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
-      *reinterpret_cast<uint2*>(dvr + d) =
-          make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+    for (int s2 = 0; s2 < NQS; ++s2) {
+      const short8_t pf = frag_tr<false>(ps, kg, s2, lane);
+      const short8_t sf = frag_tr<false>(ss, kg, s2, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dv[t] = mfma16(frag_tr<false>(ds, t, s2, lane), pf, dv[t]);
+        dk[t] = mfma16(frag_tr<false>(qs, t, s2, lane), sf, dk[t]);
+      }
+    }
+    if (kl < p.Tk) {
+      bf16_t* dkr = gg.dk + b * gg.dk_sb + h * gg.dk_sh + kl * gg.dk_st;
+      bf16_t* dvr = gg.dv + b * gg.dv_sb + h * gg.dv_sh + kl * gg.dv_st;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int d = 16 * t + 4 * Gl;
+        *reinterpret_cast<uint2*>(dkr + d) =
+            make_uint2(pack2(dk[t][0] * p.scale, dk[t][1] * p.scale),
+                       pack2(dk[t][2] * p.scale, dk[t][3] * p.scale));
+        *reinterpret_cast<uint2*>(dvr + d) =
+            make_uint2(pack2(dv[t][0], dv[t][1]), pack2(dv[t][2], dv[t][3]));
+      }
     }
   }
 }
@@ -1337,14 +1349,14 @@ GVL_DEV void bwd_short_item(const AttnP& p, const AttnG& gg, int64_t bh, const S
 // R = 32 (Tq, Tk <= 32: the cross-att decoder's 31-token self-attention, the Q-Former bridge's
 // 32 queries): 2 waves and 16 KiB of LDS per (b, h) instead of 4 waves over 64-row tiles half of
 // whose rows and waves were padding (5 blocks per CU by LDS -> 10).
-template <bool DROP, int R = 64>
-__global__ __launch_bounds__(R * 4, R == 64 ? 2 : 5) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
+template <bool DROP, int R = 64, int RK = R>
+__global__ __launch_bounds__(R * 4, R == 64 ? 2 : (RK > R ? 3 : 5)) void attn_bwd_short_kernel(AttnP p, AttnG gg) {
   const uint64_t seed_ = DROP ? seed_eff(p.seed, p.seed_ptr) : 0;
   constexpr bool L32 = GVL_ATTN_SHORT_LDS32;
-  __shared__ __attribute__((aligned(16))) char smem[L32 ? 4 : 6][R * D * 2];
-  ShortIn in;
-  bwd_short_load<DROP, R>(p, gg, blockIdx.x, in);
-  bwd_short_item<DROP, R>(p, gg, blockIdx.x, in, smem[0], seed_);
+  __shared__ __attribute__((aligned(16))) char smem[(L32 ? 2 : 4) * R * D * 2 + 2 * RK * D * 2];
+  ShortIn<2 * RK / R> in;
+  bwd_short_load<DROP, R, RK>(p, gg, blockIdx.x, in);
+  bwd_short_item<DROP, R, RK>(p, gg, blockIdx.x, in, smem, seed_);
 }
 
 int fill(const gvl_attn_desc* d, AttnP& p) {
@@ -1422,6 +1434,17 @@ bool short32_enabled() {
   return on;
 }
 
+// 32-query tiles over a 64-key tile (attn_fwd_kernel<1, *, true, 32, 64>, attn_bwd_short_kernel<*, 32,
+// 64>) for Tq <= 32 < Tk <= 64 (the cross-attention over 33 image tokens); GVL_ATTN_SHORT3264=0:
+// the 64-row kernels (A/B).
+bool short3264_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GVL_ATTN_SHORT3264");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // One-tile forward (attn_fwd_kernel<1, *, true>) for Tk <= 64; GVL_ATTN_FWD_ONE=0: the two-stage
 // kernel (A/B).
 bool fwd_one_enabled() {
@@ -1453,6 +1476,10 @@ extern "C" int gvl_attn_fwd(const gvl_attn_desc* d, gvl_stream_t stream) {
     dim3 g32(grid_1d(d, 1));
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true, 32>, g32, dim3(128), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<1, false, true, 32>, g32, dim3(128), 0, s, p);
+  } else if (d->Tq <= 32 && d->Tk <= KT && fwd_one_enabled() && short32_enabled() && short3264_enabled()) {
+    dim3 g32(grid_1d(d, 1));
+    if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true, 32, 64>, g32, dim3(128), 0, s, p);
+    else gvl::launch_timed(attn_fwd_kernel<1, false, true, 32, 64>, g32, dim3(128), 0, s, p);
   } else if (d->Tk <= KT && fwd_one_enabled()) {
     if (p.has_drop) gvl::launch_timed(attn_fwd_kernel<1, true, true>, grid, dim3(NT), 0, s, p);
     else gvl::launch_timed(attn_fwd_kernel<1, false, true>, grid, dim3(NT), 0, s, p);
@@ -1494,6 +1521,9 @@ extern "C" int gvl_attn_bwd(const gvl_attn_desc* d, const gvl_attn_bwd_desc* gd,
     if (d->Tq <= 32 && d->Tk <= 32 && short32_enabled()) {
       if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true, 32>, grid, dim3(128), 0, s, p, g);
       else gvl::launch_timed(attn_bwd_short_kernel<false, 32>, grid, dim3(128), 0, s, p, g);
+    } else if (d->Tq <= 32 && short32_enabled() && short3264_enabled()) {
+      if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true, 32, 64>, grid, dim3(128), 0, s, p, g);
+      else gvl::launch_timed(attn_bwd_short_kernel<false, 32, 64>, grid, dim3(128), 0, s, p, g);
     } else {
       if (p.has_drop) gvl::launch_timed(attn_bwd_short_kernel<true>, grid, dim3(NT), 0, s, p, g);
       else gvl::launch_timed(attn_bwd_short_kernel<false>, grid, dim3(NT), 0, s, p, g);

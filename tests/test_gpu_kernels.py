@@ -1088,12 +1088,12 @@ def test_attention_causal(cuda, B, H, T):
 
 
 @pytest.mark.parametrize("Tq,Tk", [(31, 33), (32, 32), (32, 33), (100, 257), (40, 130), (130, 1000),
-                                   (1, 32), (20, 9)])
+                                   (1, 32), (20, 9), (20, 64), (1, 40)])
 def test_attention_noncausal(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False)
 
 
-@pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130), (32, 32), (17, 29)])
+@pytest.mark.parametrize("Tq,Tk", [(32, 33), (40, 130), (32, 32), (17, 29), (31, 50)])
 def test_attention_dropout_exact_mask(cuda, Tq, Tk):
     _attn_case(cuda, 2, 2, Tq, Tk, False, packed=False, drop_p=0.1, seed=4242)
 

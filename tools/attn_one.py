@@ -26,7 +26,8 @@ def timeit(fn):
 
 for (B, H, Tq, Tk, causal, drop) in [(16, 12, 1024, 1024, True, 0.0), (128, 12, 63, 63, True, 0.0),
                                      (128, 12, 31, 31, True, 0.0),
-                                     (128, 12, 32, 32, False, 0.1), (128, 12, 32, 257, False, 0.1)]:
+                                     (128, 12, 32, 32, False, 0.1), (128, 12, 32, 257, False, 0.1),
+                                     (128, 12, 31, 33, False, 0.0), (128, 12, 32, 33, False, 0.1)]:
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = torch.randn(B, Tq, 3 * H * 64, device="cuda", generator=g).bfloat16()
     kv = torch.randn(B, Tk, 2 * H * 64, device="cuda", generator=g).bfloat16()

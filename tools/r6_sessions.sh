@@ -24,6 +24,24 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6t)  # 32-query tiles over a 64-key tile (attn_fwd_kernel<1, *, true, 32, 64>, attn_bwd_short_kernel<*, 32, 64>)
+      # for Tq <= 32 < Tk <= 64: the cross-att decoder's 31 x 33 cross-attention (12 fwd + 12 bwd per
+      # step) and the Q-Former bridge's 32 x 33. Bound: the 64-row kernels at half padding, ~16.7 us bwd
+      # + ~9 us fwd x 12 in cross -> ~25 % off = ~1 % of cross, ~0.3 % of the Q-Former step.
+      # A/B by GVL_ATTN_SHORT3264=0 (kernel stats + steps).
+  ktests kt "attention or attn"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or cross" tests/test_gpu_parity_bench.py
+  ktests full "qformer or cross" tests/test_gpu_parity_full.py
+  for v in 0 1; do
+    GVL_ATTN_SHORT3264=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s$v -o s$v -- \
+      python tools/attn_one.py 50 > $O/prof_s$v.log 2>&1; fatal $? prof_s$v
+    f=$(find $O/prof_s$v -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 14 > $O/table_s$v.txt
+    echo "== SHORT3264=$v"; grep -E "short|fwd_kernel" $O/table_s$v.txt
+  done
+  for r in 1 2 3; do for v in 0 1; do
+    GVL_ATTN_SHORT3264=$v bench cross_s${v}_$r cross; GVL_ATTN_SHORT3264=$v bench qf_s${v}_$r qformer
+  done; done
+  ;;
 r6s)  # 16 KiB short attention backward (attn_bwd_short16_kernel: never more than two 64-row tiles in LDS,
       # 76 VGPRs) for 32 < T <= 64: 6 blocks per CU instead of 5, the 1536 (b, h) blocks of the
       # Q-Former / linear decoders in one round. Bound: attn_bwd_short<false, 64> is 3.4 % of the
