@@ -24,6 +24,14 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6u)  # gate backward with its final sum in the same launch (last block by ticket): the cross-att step's 12
+      # gate_finish dispatches (~4.5 us each for 1 KiB of work) gone. Bound: 54 us of the 6.2 ms step
+      # = ~0.9 %. A/B by GVL_GATE_FUSED=0.
+  ktests kt "gate or colsum or dropout"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "cross" tests/test_gpu_parity_bench.py
+  ktests full "cross" tests/test_gpu_parity_full.py
+  for r in 1 2 3; do for v in 0 1; do GVL_GATE_FUSED=$v bench cross_g${v}_$r cross; done; done
+  ;;
 r6t)  # 32-query tiles over a 64-key tile (attn_fwd_kernel<1, *, true, 32, 64>, attn_bwd_short_kernel<*, 32, 64>)
       # for Tq <= 32 < Tk <= 64: the cross-att decoder's 31 x 33 cross-attention (12 fwd + 12 bwd per
       # step) and the Q-Former bridge's 32 x 33. Bound: the 64-row kernels at half padding, ~16.7 us bwd
