@@ -24,7 +24,7 @@ epilogue (ABI v14 act 5) -> fc2 GEMM with bias + residual.  The stock tower runs
 as separate q / k / v GEMMs, SDPA and five elementwise passes over the 32896 x 4096 fc1 output
 and the residual stream (quick-GELU as mul, sigmoid, mul; two residual adds):
 profiles/r6/clip_stock_kernel_table_r6g.txt.  Checked against the stock tower on the same
-weights (tests/test_gpu_models.py::test_clip_native_matches_stock).
+weights (tests/test_gpu_decode.py::test_clip_native_matches_stock).
 """
 from __future__ import annotations
 
