@@ -24,6 +24,13 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6v)  # PMC of the direct-A N = 768 dX launches at K = 768 and 3072 (8064 rows): where the ~0.5 us per
+      # 32-deep K-step (3.2x its MFMA time) goes — evidence for the next round's plan, no code change
+  timeout -k 10 600 bash tools/pmc_gemm.sh w4d_r6v "8064 768 768 0 1 3 -1" "8064 768 3072 0 1 3 -1"; fatal $? pmc
+  for c in 1 2; do for pn in 1 2 3; do echo "== case $c pass $pn"; python tools/pmc_summary.py gpurun_out/pmc_w4d_r6v/c${c}_p$pn; done; done > $O/pmc_summary.txt 2>&1
+  cat $O/pmc_summary.txt
+  cat gpurun_out/pmc_w4d_r6v/times.log | grep -v amdgpu.ids
+  ;;
 r6u)  # gate backward with its final sum in the same launch (last block by ticket): the cross-att step's 12
       # gate_finish dispatches (~4.5 us each for 1 KiB of work) gone. Bound: 54 us of the 6.2 ms step
       # = ~0.9 %. A/B by GVL_GATE_FUSED=0.
