@@ -24,6 +24,18 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6w)  # direct-A N = 768 dX on 128-row tiles with two workgroups per CU (gemm_w4d2_kernel, 254 VGPRs;
+      # GVL_W4D_2WG=1, plain epilogue only). Bound (r6v PMC): one wave per SIMD, 38-41 % of wave
+      # cycles in s_waitcnt, MFMA busy 0.15-0.28; the dX class is 16 % of the Q-Former step -> if a
+      # second wave per SIMD lifts MFMA busy by half, ~4-5 % of the step.
+  GVL_W4D_2WG=1 ktests kt "w4 or caption or linear_decoder or strided"
+  for r in 1 2; do for v in 0 1; do for K in 768 2304 3072; do
+    GVL_W4D_2WG=$v timeout -k 10 120 python tools/gemm_one.py 8064 768 $K 0 1 3 -1 20 > $O/g_${v}_${K}_$r.log 2>&1; fatal $? g
+    echo "2wg=$v K=$K $r $(grep -v amdgpu.ids $O/g_${v}_${K}_$r.log | tail -1)"
+  done; done; done
+  GVL_W4D_2WG=1 GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or linear" tests/test_gpu_parity_bench.py
+  for r in 1 2; do for v in 0 1; do GVL_W4D_2WG=$v bench qf_w${v}_$r qformer; done; done
+  ;;
 r6v)  # PMC of the direct-A N = 768 dX launches at K = 768 and 3072 (8064 rows): where the ~0.5 us per
       # 32-deep K-step (3.2x its MFMA time) goes — evidence for the next round's plan, no code change
   timeout -k 10 600 bash tools/pmc_gemm.sh w4d_r6v "8064 768 768 0 1 3 -1" "8064 768 3072 0 1 3 -1"; fatal $? pmc
