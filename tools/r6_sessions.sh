@@ -24,6 +24,19 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6x)  # s_setprio(1) around the T > 64 attention kernels' MFMA clusters (libgvl_prio.so, GVL_ATTN_PRIO=1):
+      # the guide's T5 (null to +6 % where hipcc moves MFMAs across barriers). Bound: attention is
+      # 14 % of the LM step -> a few % of it = ~0.3-0.8 %. attn_one + LM alternated.
+  for r in 1 2; do for v in base prio; do
+    L=$LIBDIR/libgvl.so; [ $v = prio ] && L=$LIBDIR/libgvl_prio.so
+    GVL_LIB=$L timeout -k 10 200 python -u tools/attn_one.py 20 > $O/attn_${v}_$r.log 2>&1; fatal $? attn_$v
+    echo "== attn $v $r"; grep -v amdgpu.ids $O/attn_${v}_$r.log | head -1
+  done; done
+  for r in 1 2; do for v in base prio; do
+    L=$LIBDIR/libgvl.so; [ $v = prio ] && L=$LIBDIR/libgvl_prio.so
+    GVL_LIB=$L bench lm_${v}_$r lm
+  done; done
+  ;;
 r6w)  # direct-A N = 768 dX on 128-row tiles with two workgroups per CU (gemm_w4d2_kernel, 254 VGPRs;
       # GVL_W4D_2WG=1, plain epilogue only). Bound (r6v PMC): one wave per SIMD, 38-41 % of wave
       # cycles in s_waitcnt, MFMA busy 0.15-0.28; the dX class is 16 % of the Q-Former step -> if a
