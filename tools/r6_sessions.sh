@@ -24,6 +24,16 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6y)  # rehearsal of the driver's N = 2 bench path on the one-GPU box (GVL_BENCH_ONE_DEVICE=1: both ranks
+      # on cuda:0, collectives over gloo; never a bench line): the DP buckets, the max-over-ranks
+      # timing and the library-owned teardown (gvl.dist.destroy_process_group) end to end
+  for w in qformer lm; do
+    a="--workload $w --steps 2 --warmup 1"; [ $w = lm ] && a="--steps 1 --warmup 1 --no-secondary"
+    GVL_BENCH_ONE_DEVICE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 $a --no-cpu-baseline > $O/n2_$w.json 2> $O/n2_$w.err
+    rc=$?; echo "n2 $w rc=$rc $(tail -c 400 $O/n2_$w.json)"; fatal $rc n2_$w
+  done
+  ;;
 r6x)  # s_setprio(1) around the T > 64 attention kernels' MFMA clusters (libgvl_prio.so, GVL_ATTN_PRIO=1):
       # the guide's T5 (null to +6 % where hipcc moves MFMAs across barriers). Bound: attention is
       # 14 % of the LM step -> a few % of it = ~0.3-0.8 %. attn_one + LM alternated.
