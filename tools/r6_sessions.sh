@@ -24,6 +24,23 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6z)  # residual folded into the direct-A kernel's accumulators (GVL_W4D_FOLD, as the LM's w4x): the
+      # caption decoders' bias + residual forward N = 768 GEMMs (22.0 / 56.1 us at K = 768 / 3072 vs
+      # the plain product's 17.9 / 49.0). Bound: w4d<false, 2> is 11.7 % of the Q-Former step; half
+      # the gap back = ~0.8 %. A/B against libgvl_nofold.so.
+  ktests kt "w4 or gated or dropout_residual or linear_decoder or caption"
+  GVL_MARGINS_DIR=$O/parity_margins ktests parity "qformer or linear" tests/test_gpu_parity_bench.py
+  ktests full "qformer" tests/test_gpu_parity_full.py
+  for r in 1 2; do for v in nofold new; do for K in 768 3072; do
+    L=$LIBDIR/libgvl.so; [ $v = nofold ] && L=$LIBDIR/libgvl_nofold.so
+    GVL_LIB=$L timeout -k 10 120 python tools/gemm_one.py 8064 768 $K 0 0 3 -1 20 bias_res > $O/g_${v}_${K}_$r.log 2>&1; fatal $? g
+    echo "$v K=$K $r $(grep -v amdgpu.ids $O/g_${v}_${K}_$r.log | tail -1)"
+  done; done; done
+  for r in 1 2 3; do for v in nofold new; do
+    L=$LIBDIR/libgvl.so; [ $v = nofold ] && L=$LIBDIR/libgvl_nofold.so
+    GVL_LIB=$L bench qf_${v}_$r qformer
+  done; done
+  ;;
 r6y)  # rehearsal of the driver's N = 2 bench path on the one-GPU box (GVL_BENCH_ONE_DEVICE=1: both ranks
       # on cuda:0, collectives over gloo; never a bench line): the DP buckets, the max-over-ranks
       # timing and the library-owned teardown (gvl.dist.destroy_process_group) end to end
