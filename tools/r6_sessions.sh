@@ -297,7 +297,7 @@ r6e)  # Q-Former floor budget inputs: every GEMM instance of
     python bench.py --workload qformer --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_qf.json 2> $O/prof_qf.err; fatal $? prof_qf
   f=$(find $O/prof_qf -name "*kernel_stats.csv" | head -1); python tools/prof_table.py $f 45 > $O/qf_table.txt; head -30 $O/qf_table.txt
   ;;
-r6fin|r6fin2|r6fin3)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
+r6fin|r6fin2|r6fin3|r6fin4)  # head check: GPU suite + smoke, the driver's default bench, rocprofv3 kernel stats of all four steps
   suite
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; fatal $? bench
   python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline']['frac'],d['roofline']['kernel'],[(k,d[k]['value']) for k in d if k.startswith('caption')])"
