@@ -11,7 +11,7 @@ for spec in "$@"; do
   i=$((i+1))
   for pn in 1 2 3; do
     eval "CTRS=\$P$pn"
-    timeout -k 10 120 rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d $OUT/c${i}_p$pn -o run -- python tools/gemm_one.py $spec 5 > $OUT/c${i}_p$pn.log 2>&1 || exit $?
+    timeout -k 10 120 rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d $OUT/c${i}_p$pn -o run -- python tools/gemm_one.py $spec 5 ${EPI:-plain} > $OUT/c${i}_p$pn.log 2>&1 || exit $?
   done
-  timeout -k 10 120 python tools/gemm_one.py $spec 20 >> $OUT/times.log 2>&1 || exit $?
+  timeout -k 10 120 python tools/gemm_one.py $spec 20 ${EPI:-plain} >> $OUT/times.log 2>&1 || exit $?
 done

@@ -24,6 +24,14 @@ bench() {  # bench <tag> <workload> [steps]   (env passes through)
   echo "$1 $(python -c "import json;d=json.load(open('$O/$1.json'));print(d['value'],d.get('step_mfma_frac'),d.get('peak_hbm_gib'))")"
 }
 case $S in
+r6pp)  # PMC of the wide K = 768 class at the Q-Former shape (8064 x 3072 x 768): c_fc + GELU with its
+       # gelu' side output (act) vs the plain product — where the un-overlapped stores' time goes
+       # (evidence for the next round's plan; no code change)
+  EPI=act timeout -k 10 600 bash tools/pmc_gemm.sh pp3act_r6pp "8064 3072 768 0 0 3 -1"; fatal $? pmc_act
+  EPI=plain timeout -k 10 600 bash tools/pmc_gemm.sh pp3plain_r6pp "8064 3072 768 0 0 3 -1"; fatal $? pmc_plain
+  for t in pp3act_r6pp pp3plain_r6pp; do for pn in 1 2 3; do echo "== $t pass $pn"; python tools/pmc_summary.py gpurun_out/pmc_$t/c1_p$pn; done; grep -v amdgpu.ids gpurun_out/pmc_$t/times.log; done > $O/pmc_summary.txt 2>&1
+  cat $O/pmc_summary.txt
+  ;;
 r6z)  # residual folded into the direct-A kernel's accumulators (GVL_W4D_FOLD, as the LM's w4x): the
       # caption decoders' bias + residual forward N = 768 GEMMs (22.0 / 56.1 us at K = 768 / 3072 vs
       # the plain product's 17.9 / 49.0). Bound: w4d<false, 2> is 11.7 % of the Q-Former step; half
